@@ -1,0 +1,159 @@
+/* yrt_device.h — C ABI of the MI355X path-tracing device plugin (libdevice_singleray_mi355x.so).
+ *
+ * This is the reference's device plugin boundary made C-callable. Each entry point
+ * replaces one virtual method of embree::Device (devices/device/device.h:51-330) with the
+ * same arguments and semantics; the plugin factory replaces
+ * `extern "C" Device* create(const char* parms, size_t numThreads, int threadsPriority,
+ * const char* rtcore_cfg)` (devices/device_singleray/api/singleray_device.cpp:105-107,
+ * resolved by devices/device/device.cpp:24-35).
+ *
+ * Conventions
+ *   - Handles are opaque pointers to ref-counted objects starting at refcount 1
+ *     (device_singleray/api/handle.h:26-31). yrtIncRef/yrtDecRef mirror rtIncRef/rtDecRef.
+ *   - rtSet* values are buffered; yrtCommit (re)constructs the object (api/handle.h:99-103).
+ *   - The reference throws std::runtime_error; here every call returns 0 on success and a
+ *     negative code on failure, with the message in yrtGetLastError(device). No exception
+ *     crosses the ABI.
+ *   - Every call on one device is serialized by a device mutex (singleray_device.cpp:97).
+ *   - yrtRenderFrame is synchronous (integratorrenderer.cpp:90-93); yrtMapFrameBuffer
+ *     returns the host pixel pointer (singleray_device.cpp:439-447).
+ */
+#ifndef YRT_DEVICE_H
+#define YRT_DEVICE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YRT_API __attribute__((visibility("default")))
+
+typedef struct YRTDevice_* YRTDevice;
+typedef void* YRTHandle;
+
+/* ---- device lifetime (Device::rtCreateDevice / create) ------------------------------ */
+/* parms: "" or "device=N" to pick a HIP device; "host" creates a host-only device (loaders,
+ * scene commit, BVH build, yrtExportFrame/BVH; rendering and ray queries fail) used by the
+ * CPU test suite. numThreads / threadsPriority are accepted
+ * for signature parity (they size the CPU TaskScheduler in the reference and are unused
+ * on the GPU). */
+YRT_API YRTDevice yrtNewDevice(const char* parms, size_t numThreads, int threadsPriority, const char* rtcore_cfg);
+YRT_API void yrtDeleteDevice(YRTDevice dev);
+YRT_API const char* yrtGetLastError(YRTDevice dev);
+
+/* ---- object creation (device.h:126-214) ---------------------------------------------- */
+YRT_API YRTHandle yrtNewCamera(YRTDevice dev, const char* type);        /* "pinhole", "stereo" */
+YRT_API YRTHandle yrtNewData(YRTDevice dev, const char* type, size_t bytes, const void* data);
+YRT_API YRTHandle yrtNewImage(YRTDevice dev, const char* type, size_t width, size_t height, const void* data);
+                                                                       /* "RGB8","RGBA8","RGB_FLOAT32","RGBA_FLOAT32" */
+YRT_API YRTHandle yrtNewImageFromFile(YRTDevice dev, const char* file); /* .ppm/.png/.jpg */
+YRT_API YRTHandle yrtNewTexture(YRTDevice dev, const char* type);       /* "bilinear","nearest","image" */
+YRT_API YRTHandle yrtNewMaterial(YRTDevice dev, const char* type);
+YRT_API YRTHandle yrtNewShape(YRTDevice dev, const char* type);         /* "trianglemesh","sphere","triangle" */
+YRT_API YRTHandle yrtNewLight(YRTDevice dev, const char* type);         /* "ambientlight","trianglelight","hdrilight" */
+YRT_API YRTHandle yrtNewShapePrimitive(YRTDevice dev, YRTHandle shape, YRTHandle material, const float* transform12,
+                                       int faceCamera);
+YRT_API YRTHandle yrtNewLightPrimitive(YRTDevice dev, YRTHandle light, YRTHandle material, const float* transform12);
+YRT_API YRTHandle yrtNewScene(YRTDevice dev, const char* type);
+YRT_API int yrtSetPrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim);
+YRT_API YRTHandle yrtNewToneMapper(YRTDevice dev, const char* type);    /* "default" */
+YRT_API YRTHandle yrtNewRenderer(YRTDevice dev, const char* type);      /* "pathtracer", "debug" */
+YRT_API YRTHandle yrtNewFrameBuffer(YRTDevice dev, const char* type, size_t width, size_t height, size_t buffers,
+                                    void** ptrs);
+
+/* ---- reference counting / properties (device.h:237-312) ----------------------------- */
+YRT_API int yrtIncRef(YRTDevice dev, YRTHandle h);
+YRT_API int yrtDecRef(YRTDevice dev, YRTHandle h);
+YRT_API int yrtSetBool1(YRTDevice dev, YRTHandle h, const char* property, int x);
+YRT_API int yrtSetInt1(YRTDevice dev, YRTHandle h, const char* property, int x);
+YRT_API int yrtSetInt2(YRTDevice dev, YRTHandle h, const char* property, int x, int y);
+YRT_API int yrtSetInt3(YRTDevice dev, YRTHandle h, const char* property, int x, int y, int z);
+YRT_API int yrtSetInt4(YRTDevice dev, YRTHandle h, const char* property, int x, int y, int z, int w);
+YRT_API int yrtSetFloat1(YRTDevice dev, YRTHandle h, const char* property, float x);
+YRT_API int yrtSetFloat2(YRTDevice dev, YRTHandle h, const char* property, float x, float y);
+YRT_API int yrtSetFloat3(YRTDevice dev, YRTHandle h, const char* property, float x, float y, float z);
+YRT_API int yrtSetFloat4(YRTDevice dev, YRTHandle h, const char* property, float x, float y, float z, float w);
+YRT_API int yrtGetFloat3(YRTDevice dev, YRTHandle h, const char* property, float* x, float* y, float* z);
+YRT_API int yrtSetArray(YRTDevice dev, YRTHandle h, const char* property, const char* type, YRTHandle data,
+                        size_t size, size_t stride, size_t ofs);
+YRT_API int yrtSetString(YRTDevice dev, YRTHandle h, const char* property, const char* str);
+YRT_API int yrtSetImage(YRTDevice dev, YRTHandle h, const char* property, YRTHandle image);
+YRT_API int yrtSetTexture(YRTDevice dev, YRTHandle h, const char* property, YRTHandle texture);
+YRT_API int yrtSetTransform(YRTDevice dev, YRTHandle h, const char* property, const float* transform12);
+YRT_API int yrtSetPointer(YRTDevice dev, YRTHandle h, const char* property, void* p);
+YRT_API int yrtClear(YRTDevice dev, YRTHandle h);
+YRT_API int yrtCommit(YRTDevice dev, YRTHandle h);
+
+/* ---- rendering (device.h:223-234, 322) ----------------------------------------------- */
+YRT_API int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene,
+                           YRTHandle tonemapper, YRTHandle framebuffer, int accumulate);
+YRT_API void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
+YRT_API int yrtUnmapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
+YRT_API int yrtSwapBuffers(YRTDevice dev, YRTHandle framebuffer);
+/* Renderer status callback (device.h:335-347): state 0 Inactive, 1 Rendering, 2 Done. */
+typedef void (*YRTStatusCallback)(int state, float progress, void* user);
+YRT_API int yrtSetStatusCallback(YRTDevice dev, YRTHandle renderer, YRTStatusCallback cb, void* user);
+/* Stop flag polled between wavefront iterations (renderer "stopFlag", integratorrenderer.h:100). */
+YRT_API int yrtSetStopFlag(YRTDevice dev, YRTHandle renderer, volatile int* flag);
+
+/* ---- hot-path ray queries: rtcIntersect / rtcOccluded over device-resident streams ---- */
+/* org4[i] = (org.xyz, tnear), dir4[i] = (dir.xyz, tfar) ; hit4[i] = (t, u, v, triId bits)
+ * occluded[i] = 1/0. All pointers are HIP device pointers; stream may be NULL (default).
+ * Replaces rtcIntersect (pathtraceintegrator.cpp:72) and rtcOccluded (:160). */
+YRT_API int yrtIntersect(YRTDevice dev, YRTHandle scene, const float* org4, const float* dir4, uint32_t n,
+                         float* hit4, void* stream);
+YRT_API int yrtOccluded(YRTDevice dev, YRTHandle scene, const float* org4, const float* dir4, uint32_t n,
+                        int32_t* occluded, void* stream);
+/* Maps a global triangle id (hit4.w) to Embree's (geomID, primID). */
+YRT_API int yrtTriangleIds(YRTDevice dev, YRTHandle scene, int32_t tri, int32_t* geomID, int32_t* primID);
+
+/* ---- statistics of the last yrtRenderFrame (integratorrenderer.cpp:96-116) ------------ */
+typedef struct YRTRenderStats {
+  double raysClosest;     /* rtcIntersect-equivalent queries  */
+  double raysShadow;      /* rtcOccluded-equivalent queries   */
+  double samples;         /* W*H*spp                          */
+  double msTotal;         /* wall time of yrtRenderFrame      */
+  double msTraceClosest;  /* summed kernel time (HIP events) when timing enabled */
+  double msTraceShadow;
+  double msShade;
+  double msOther;
+  double launchesClosest; /* kernel launches of each kind */
+  double launchesShadow;
+  double nodeVisits;      /* reserved (0): visit counts come from oracle_count_visits */
+  double triVisits;
+} YRTRenderStats;
+YRT_API int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out);
+/* 1 = bracket every kernel with HIP events (adds sync-free event records). */
+YRT_API int yrtSetKernelTiming(YRTDevice dev, int enable);
+/* Scene info: triangles, geometries, BVH nodes, BVH depth, build seconds. */
+typedef struct YRTSceneInfo {
+  int64_t numTriangles, numGeometries, numNodes, bvhDepth, numLights;
+  double buildSeconds;
+  float bboxLo[3], bboxHi[3];
+} YRTSceneInfo;
+YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
+/* Copies the host mirror of the BVH (nodes: 64 B each, tris: 48 B each) for tests. */
+YRT_API int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes, void* tris,
+                         size_t trisBytes);
+/* Serializes the committed scene graph + renderer + camera as the oracle's input blob
+ * (format: oracle/yrt_oracle.h). Returns the byte count; call with buf=NULL to size. */
+YRT_API int64_t yrtExportFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene, void* buf,
+                               size_t bytes);
+/* Frame seed of the shadow-jitter hash (replaces C rand(), pathtraceintegrator.cpp:151). */
+YRT_API int yrtSetFrameSeed(YRTDevice dev, uint32_t seed);
+/* Paths in flight per wavefront batch (default 16M); smaller for tests. */
+YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
+/* Tile sharding for multi-GPU: render only tiles with (tileIndex % count) == index. */
+YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
+/* Host sampler check: writes the SoA sample table (dims x (sets*spp)) that the frame
+ * renderer uploads (sampler/sampler.cpp:46-126 restated); returns sets*spp records. */
+YRT_API int yrtDebugSampleTable(int spp, int sets, int iteration, int num1D, int num2D, const char* filter,
+                                float* out, size_t outFloats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YRT_DEVICE_H */

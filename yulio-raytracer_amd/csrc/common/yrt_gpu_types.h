@@ -1,0 +1,122 @@
+// yrt_gpu_types.h — HBM layout of a committed scene and of the wavefront path state.
+//
+// Everything the kernels read is a flat array uploaded once per rtCommit(scene)
+// (the reference rebuilt the Embree BVH at every commit, api/scene_flat.h:72-97).
+//
+//  BVH (binary, SAH, built on the host — device/bvh_build.cpp):
+//    GpuNode   64 B  both children's AABBs + (child, count) pairs, Aila-Laine style so
+//                    one 64-B line serves the two box tests of a traversal step.
+//    GpuTri    48 B  Embree-convention Moeller-Trumbore triangle in leaf order:
+//                    v0, e1 = v0-v1, e2 = v2-v0 (rtcore triangle convention);
+//                    v0.w = global triangle id (int bits), e1.w = flags (cull bit).
+//  Shading (indexed by global triangle id = geomTriBase[geomID] + primID):
+//    triGeom   int   geomID of every triangle
+//    indices   int4  (v0,v1,v2, -) absolute vertex ids
+//    positions float4, normals float4, texcoords float2 (world space, per vertex)
+//    GpuGeom, GpuMaterial, GpuTexture/GpuImage, GpuLight tables.
+#pragma once
+
+#include <stdint.h>
+
+namespace yrt {
+
+enum GeomKind : int32_t { GEOM_MESH_FULL = 0, GEOM_MESH_NORMALS = 1, GEOM_TRIANGLE = 2 };
+enum GeomFlags : int32_t { GF_NORMALS = 1, GF_TEXCOORDS = 2, GF_CULL = 4 };
+
+struct GpuNode {
+  float b0[4];  // c0.lo.x c0.hi.x c0.lo.y c0.hi.y
+  float b1[4];  // c1.lo.x c1.hi.x c1.lo.y c1.hi.y
+  float b2[4];  // c0.lo.z c0.hi.z c1.lo.z c1.hi.z
+  int32_t c[4]; // child0, child1, count0, count1 (count 0: inner node index; >0: leaf tri range)
+};
+static_assert(sizeof(GpuNode) == 64, "node is one 64-B line");
+
+struct GpuTri {
+  float v0[4];  // xyz, w = global triangle id (bits)
+  float e1[4];  // xyz, w = flags (bits): bit0 cullBackFaces
+  float e2[4];  // xyz, w unused
+};
+static_assert(sizeof(GpuTri) == 48, "tri record is 48 B");
+
+struct GpuGeom {
+  int32_t kind, material, light, flags;
+  int32_t vtxBase, triBase, illumMask, shadowMask;
+  float Ng[4];  // GEOM_TRIANGLE: normalized cross(v2-v0, v1-v0) (shapes/triangle.h:28)
+};
+
+enum MaterialType : int32_t {
+  MAT_NONE = 0,
+  MAT_MATTE = 1,
+  MAT_MATTE_TEXTURED = 2,
+  MAT_METALLIC_PAINT = 3,
+  MAT_OBJ = 4,
+  MAT_UBER = 5,
+  MAT_THIN_DIELECTRIC = 6,
+};
+
+// Parameter slots per material type (filled by device/materials.cpp from Parms with the
+// reference constructors' defaults).
+struct GpuMaterial {
+  int32_t type;
+  int32_t tex[5];   // texture ids (-1 none). Uber/MatteTextured/ThinDielectric: tex[0]=Kd.
+                    // Obj: map_d, map_Kd, map_Ks, map_Ns, map_Bump
+  int32_t pad[2];
+  float p[24];
+};
+
+enum TexFilter : int32_t { TEX_BILINEAR = 0, TEX_NEAREST = 1 };
+// IMG_RGBA8: Image4c (alpha = byte/255); IMG_RGB8: Image3c stored as RGBA8 whose alpha
+// reads as exactly 1.0f (common/math/color_scalar.h:45); IMG_RGBAF32: Image3f/4f.
+enum ImageFormat : int32_t { IMG_RGBA8 = 0, IMG_RGBAF32 = 1, IMG_RGB8 = 2 };
+struct GpuImage {
+  int32_t width, height, format, pad;
+  int64_t offset;   // byte offset into the texel pool
+};
+struct GpuTexture {
+  int32_t image, filter, invert, pad;
+};
+
+enum LightType : int32_t { LIGHT_AMBIENT = 0, LIGHT_TRIANGLE = 1, LIGHT_HDRI = 2 };
+struct GpuLight {
+  int32_t type, illumMask, shadowMask, precomputed;  // precomputed: index into light-sample slots or -1
+  int32_t isEnv, image, distOffset, pad;             // HDRI: image id, distribution offset (floats)
+  float L[4];
+  float v0[4], v1[4], v2[4];     // triangle light vertices
+  float e1[4], e2[4], Ng[4];     // e1 = v0-v1, e2 = v2-v0, Ng = cross(e1,e2) (lights/trianglelight.h:24)
+  float bsphere[4];              // ambient: center.xyz, radius (ambientlight.h:28-32)
+  float l2w[12], w2l[12];        // HDRI local2world / world2local (column-major l, then p)
+  int32_t hdriW, hdriH, pad2[2];
+};
+
+// Renderer parameters (integrators/pathtraceintegrator.cpp:21-33 defaults).
+struct GpuRenderParams {
+  int32_t maxDepth, rrDepth, spp, sets;
+  float minContribution, epsilon, tMaxShadowRay, tMaxShadowJitter;
+  float up[4];
+  int32_t numLights, numEnvLights, numPrecomp, dim1D;  // dim1D = maxDepth
+  int32_t dim2D, lightSampleID, firstScatterSampleID, firstScatterTypeSampleID;
+  int32_t width, height, numTilesX, numTilesY;
+  float rcpWidth, rcpHeight, gamma, rcpGamma;
+  uint32_t frameSeed, pad[3];
+};
+
+// Camera (cameras/pinholecamera.h:15-21, cameras/StereoCubeCamera.h:16-65).
+enum CameraType : int32_t { CAM_PINHOLE = 0, CAM_STEREO = 1 };
+struct GpuCamera {
+  int32_t type, cubeFaceIndex, toeIn, pad;
+  float p2w[6][12];           // pixel2world[face]: vx, vy, vz, p (column-major)
+  float origin[4], up[4], xyzStraight[4];
+  float eyeSeparation, rcpZeroParallaxDistance, falloffAngle, pad2;
+};
+
+// Precomputed sample table (samplers/sampler.cpp:85-158), SoA [dim][set*spp + s].
+//   dims: 0,1 pixel.xy | 2,3 lens | 4 time | 5.. 1D (dim1D) | then 2D (dim2D x 2)
+//   light samples (HDRI precompute): per slot 8 floats (wi.xyz, pdf, L.rgb, tMax)
+struct SampleTableLayout {
+  int32_t numRecords;   // sets * spp
+  int32_t numDims;      // 5 + dim1D + 2*dim2D
+  int32_t numLightSlots;
+  int32_t pad;
+};
+
+}  // namespace yrt

@@ -1,0 +1,22 @@
+// bvh_build.h — host BVH2 builder (see bvh_build.cpp).
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "../common/yrt_gpu_types.h"
+
+namespace yrt {
+
+struct BvhResult {
+  std::vector<GpuNode> nodes;
+  std::vector<GpuTri> tris;   // leaf order
+  std::vector<int> order;     // leaf slot -> global triangle id
+  int maxDepth = 0;
+};
+
+// v: 9 floats (v0,v1,v2) per global triangle id; flags: per-triangle GpuTri flags (bit0 cull)
+void build_bvh(const std::vector<float>& v, const std::vector<uint32_t>& flags, int stackDepth, BvhResult& out);
+
+}  // namespace yrt

@@ -1,0 +1,879 @@
+// device.cpp — the MI355X device plugin: C-ABI entry points (include/yrt_device.h) over the
+// object model, scene commit and the wavefront frame renderer.
+//
+// Reference counterparts: SingleRayDevice (device_singleray/api/singleray_device.cpp:99-709),
+// IntegratorRenderer::renderFrame/RenderJob (renderers/integratorrenderer.cpp:63-185),
+// DebugRenderer (renderers/debugrenderer.cpp:66-140).
+#include "../../../include/yrt_device.h"
+
+#include <string.h>
+#include <strings.h>
+
+#include <chrono>
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+
+#include "../kernels/yrt_kernels.h"
+#include "image_io.h"
+#include "objects.h"
+#include "scene_gpu.h"
+#include "sampler.h"
+
+namespace yrt {
+
+#ifndef YRT_STACK_DEPTH
+#define YRT_STACK_DEPTH 40
+#endif
+
+struct FrameCache {
+  std::string key;
+  SampleTable table;
+  DevBuf dims, light;
+};
+
+class Device {
+ public:
+  std::recursive_mutex mu;
+  std::string lastError;
+  std::set<HandleRef*> handles;
+  int hipDevice = 0;
+  hipStream_t stream = nullptr;
+  uint32_t frameSeed = 0x2545F491u;
+  int64_t capacity = 16ll << 20;
+  int shardIndex = 0, shardCount = 1;
+  bool kernelTiming = false;
+  YRTRenderStats stats{};
+
+  // per-frame device state
+  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCounters, dCount;
+  DevBuf qPath[2], qOrg[2], qDir[2], hit, thr, L, meta, shFirst, sOrg, sDir, sContrib, sOcc;
+  int64_t pathCap = 0, shadowCap = 0;
+  FrameCache fcache;
+  std::vector<hipEvent_t> eventPool;
+
+  bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
+  explicit Device(int dev, bool useGpu) : hipDevice(dev), gpu(useGpu) {
+    if (!gpu) return;
+    HIP_CHECK(hipSetDevice(hipDevice));
+    HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  }
+  ~Device() {
+    for (auto* h : handles) delete h;
+    for (auto e : eventPool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  YRTHandle wrap(std::shared_ptr<Object> o) {
+    o->dev = this;
+    auto* h = new HandleRef();
+    h->obj = std::move(o);
+    handles.insert(h);
+    return (YRTHandle)h;
+  }
+  HandleRef* ref(YRTHandle h) {
+    auto* r = (HandleRef*)h;
+    if (!r || handles.find(r) == handles.end()) throw std::runtime_error("invalid handle");
+    return r;
+  }
+  template <class T>
+  std::shared_ptr<T> get(YRTHandle h, const char* what) {
+    if (!h) return nullptr;
+    auto o = std::dynamic_pointer_cast<T>(ref(h)->obj);
+    if (!o) throw std::runtime_error(std::string("invalid ") + what + " handle");
+    return o;
+  }
+
+  void ensure_paths(int64_t P, int numLights) {
+    if (P > pathCap) {
+      for (int k = 0; k < 2; ++k) {
+        qPath[k].alloc(P * 4);
+        qOrg[k].alloc(P * 16);
+        qDir[k].alloc(P * 16);
+      }
+      hit.alloc(P * 16);
+      thr.alloc(P * 16);
+      L.alloc(P * 16);
+      meta.alloc(P * 4);
+      pathCap = P;
+    }
+    const int64_t S = P * std::max(1, numLights);
+    if (S > shadowCap) {
+      shFirst.alloc(S * 4);
+      sOrg.alloc(S * 16);
+      sDir.alloc(S * 16);
+      sContrib.alloc(S * 16);
+      sOcc.alloc(S * 4);
+      shadowCap = S;
+    }
+  }
+
+  hipEvent_t ev() {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    eventPool.push_back(e);
+    return e;
+  }
+
+  void render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F, int accumulate);
+  void intersect(SceneObj& S, const float* org4, const float* dir4, uint32_t n, float* hit4, int32_t* occ,
+                 hipStream_t st);
+};
+
+// ---------------------------------------------------------------- rendering
+static void status(RendererObj& R, int state, float progress) {
+  if (R.statusCallback) ((YRTStatusCallback)R.statusCallback)(state, progress, R.statusUser);
+}
+
+void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F,
+                    int accumulate) {
+  auto t0 = std::chrono::steady_clock::now();
+  HIP_CHECK(hipSetDevice(hipDevice));
+  if (!S.gpu) throw std::runtime_error("scene not committed");
+  if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
+  GpuScene& G = *S.gpu;
+  const int W = F.width, H = F.height;
+  memset(&stats, 0, sizeof(stats));
+
+  GpuRenderParams rp;
+  memset(&rp, 0, sizeof(rp));
+  rp.width = W;
+  rp.height = H;
+  rp.numTilesX = (W + 15) / 16;
+  rp.numTilesY = (H + 15) / 16;
+  rp.rcpWidth = rcpf_(float(W));
+  rp.rcpHeight = rcpf_(float(H));
+  rp.gamma = T.gamma;
+  rp.rcpGamma = rcpf_(T.gamma);
+  rp.frameSeed = frameSeed;
+  rp.maxDepth = R.maxDepth;
+  rp.rrDepth = R.rrDepth;
+  rp.minContribution = R.minContribution;
+  rp.epsilon = R.epsilon;
+  rp.tMaxShadowRay = R.tMaxShadowRay;
+  rp.tMaxShadowJitter = R.tMaxShadowJitter;
+  rp.up[0] = R.up.x; rp.up[1] = R.up.y; rp.up[2] = R.up.z;
+  rp.numLights = G.view.numLights;
+  rp.numEnvLights = G.view.numEnvLights;
+  rp.numPrecomp = (int)G.precomputed.size();
+
+  // samples: PathTraceIntegrator::requestSamples (pathtraceintegrator.cpp:35-47)
+  if (!accumulate) R.iteration = 0;
+  SampleRequest req;
+  req.spp = R.debug ? 1 : R.spp;
+  req.sets = R.sets;
+  req.iteration = R.iteration;
+  req.num1D = R.debug ? 0 : R.maxDepth;
+  req.num2D = R.debug ? 0 : 1 + R.maxDepth;
+  req.filter = R.filter;
+  if (!R.debug) req.lights = G.precomputed;
+  rp.dim1D = req.num1D;
+  rp.dim2D = req.num2D;
+  rp.lightSampleID = 0;
+  rp.firstScatterSampleID = 1;
+  rp.firstScatterTypeSampleID = 0;
+  char keybuf[256];
+  snprintf(keybuf, sizeof(keybuf), "%d/%d/%d/%d/%d/%s/%p", req.spp, req.sets, req.iteration, req.num1D, req.num2D,
+           req.filter.c_str(), (void*)&G);
+  if (fcache.key != keybuf) {
+    build_sample_table(req, fcache.table);
+    fcache.dims.upload(fcache.table.dims);
+    fcache.light.upload(fcache.table.light);
+    fcache.key = keybuf;
+  }
+  const SampleTable& tab = fcache.table;
+  rp.spp = tab.spp;
+  rp.sets = tab.sets;
+
+  dRp.alloc(sizeof(rp));
+  dCam.alloc(sizeof(GpuCamera));
+  HIP_CHECK(hipMemcpyAsync(dRp.p, &rp, sizeof(rp), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(dCam.p, &C.cam, sizeof(GpuCamera), hipMemcpyHostToDevice, stream));
+  dPixelSets.alloc((size_t)W * H);
+  const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
+  dFbFloat.alloc((size_t)W * H * 3 * sizeof(float));
+  dFbRGB8.alloc(rgb8Stride * H);
+
+  FrameView fv;
+  fv.rp = dRp.as<GpuRenderParams>();
+  fv.cam = dCam.as<GpuCamera>();
+  fv.samples = fcache.dims.as<float>();
+  fv.lightSamples = fcache.light.as<float>();
+  fv.pixelSets = dPixelSets.as<uint8_t>();
+  fv.numRecords = tab.numRecords;
+  fv.numLightSlots = std::max(1, tab.numLightSlots);
+
+  status(R, 1, 0.f);
+  const int numTiles = rp.numTilesX * rp.numTilesY;
+  // tiles of this shard: tile = shardIndex + k * shardCount
+  const int shardTiles = numTiles > shardIndex ? (numTiles - shardIndex + shardCount - 1) / shardCount : 0;
+
+  if (R.debug) {
+    launch_debug_render(G.view, fv, R.maxDepth, R.spp, numTiles, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(),
+                        (int)rgb8Stride, stream);
+    stats.raysClosest = 0;
+  } else {
+    launch_pixel_sets(fv, dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
+    const int spp = rp.spp;
+    int64_t tilesPerBatch = std::max<int64_t>(1, capacity / (256ll * spp));
+    const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
+    ensure_paths(std::max<int64_t>(P, 256ll * spp), rp.numLights);
+    const int levels = rp.maxDepth + 1;
+    dCounters.alloc((size_t)levels * 4 * sizeof(unsigned));
+    dAccu.alloc((size_t)W * H * 16);
+    std::vector<unsigned> hc(levels * 4);
+    PathBuffers pb;
+    for (int k = 0; k < 2; ++k) {
+      pb.qPath[k] = qPath[k].as<int>();
+      pb.qOrg[k] = qOrg[k].as<float4>();
+      pb.qDir[k] = qDir[k].as<float4>();
+    }
+    pb.hit = hit.as<float4>();
+    pb.thr = thr.as<float4>();
+    pb.L = L.as<float4>();
+    pb.meta = meta.as<int>();
+    pb.shFirst = shFirst.as<int>();
+    pb.sOrg = sOrg.as<float4>();
+    pb.sDir = sDir.as<float4>();
+    pb.sContrib = sContrib.as<float4>();
+    pb.sOcc = sOcc.as<int>();
+    pb.counters = dCounters.as<unsigned>();
+    pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
+    pb.shadowCapacity = (int)(pb.capacity * std::max(1, rp.numLights));
+
+    struct EvPair { hipEvent_t a, b; int kind; };
+    std::vector<EvPair> evs;
+    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch) {
+      if (R.stopFlag && R.stopFlag->load()) break;
+      BatchInfo bi;
+      bi.firstTile = (int)first;
+      bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
+      bi.tileStride = shardCount;
+      bi.tileOffset = shardIndex;
+      HIP_CHECK(hipMemsetAsync(dCounters.p, 0, (size_t)levels * 4 * sizeof(unsigned), stream));
+      launch_raygen(fv, pb, bi, stream);
+      for (int d = 0; d < rp.maxDepth; ++d) {
+        const int cur = d & 1;
+        EvPair e1{};
+        if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, stream)); }
+        launch_trace_closest(G.view, pb.qOrg[cur], pb.qDir[cur], pb.counters + d * 4, pb.capacity, pb.hit, stream);
+        if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, stream)); evs.push_back(e1); }
+        EvPair e2{};
+        if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
+        launch_shade(G.view, fv, pb, bi, d, stream);
+        if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, stream)); evs.push_back(e2); }
+        if (rp.numLights > 0) {
+          EvPair e3{};
+          if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
+          launch_trace_any(G.view, pb.sOrg, pb.sDir, pb.counters + d * 4 + 1, pb.shadowCapacity, pb.sOcc, stream);
+          if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
+          launch_shadow_resolve(pb, d, rp.numLights, stream);
+        }
+      }
+      launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
+                            dAccu.as<float4>(), accumulate ? 1 : 0, stream);
+      HIP_CHECK(hipMemcpyAsync(hc.data(), dCounters.p, hc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+      for (int d = 0; d < levels; ++d) {
+        stats.raysClosest += hc[d * 4 + 0];
+        stats.raysShadow += hc[d * 4 + 1];
+        if (d < rp.maxDepth && hc[d * 4 + 0]) stats.launchesClosest += 1;
+        if (d < rp.maxDepth && hc[d * 4 + 1]) stats.launchesShadow += 1;
+      }
+      status(R, 1, float(first + bi.numPixels / 256) / float(std::max(1, shardTiles)));
+    }
+    for (auto& e : evs) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));
+      if (e.kind == 0) stats.msTraceClosest += ms;
+      else if (e.kind == 1) stats.msTraceShadow += ms;
+      else stats.msShade += ms;
+    }
+    for (auto e : eventPool) (void)hipEventDestroy(e);
+    eventPool.clear();
+    R.iteration++;
+  }
+  HIP_CHECK(hipStreamSynchronize(stream));
+
+  // framebuffer write-back (api/framebuffer.h:93-226)
+  void* dst = F.buffer(F.cur);
+  if (F.format == FB_RGB8) {
+    HIP_CHECK(hipMemcpy(dst, dFbRGB8.p, rgb8Stride * H, hipMemcpyDeviceToHost));
+  } else {
+    std::vector<float> tmp((size_t)W * H * 3);
+    HIP_CHECK(hipMemcpy(tmp.data(), dFbFloat.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+    if (F.format == FB_RGB_FLOAT32) {
+      memcpy(dst, tmp.data(), tmp.size() * sizeof(float));
+    } else if (F.format == FB_RGBA_FLOAT32) {
+      float* o = (float*)dst;
+      for (size_t i = 0; i < (size_t)W * H; ++i) {
+        o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
+      }
+    } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
+      uint8_t* o = (uint8_t*)dst;
+      for (size_t i = 0; i < (size_t)W * H; ++i) {
+        for (int k = 0; k < 3; ++k) o[4 * i + k] = (uint8_t)clampf(tmp[3 * i + k] * 255.0f, 0.0f, 255.0f);
+        o[4 * i + 3] = 0;
+      }
+    }
+  }
+  stats.samples = (double)W * H * rp.spp;
+  stats.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  status(R, 2, 1.f);
+}
+
+// ---------------------------------------------------------------- ray queries
+void Device::intersect(SceneObj& S, const float* org4, const float* dir4, uint32_t n, float* hit4, int32_t* occ,
+                       hipStream_t st) {
+  HIP_CHECK(hipSetDevice(hipDevice));
+  if (!S.gpu) throw std::runtime_error("scene not committed");
+  dCount.alloc(sizeof(unsigned));
+  HIP_CHECK(hipMemcpyAsync(dCount.p, &n, sizeof(unsigned), hipMemcpyHostToDevice, st));
+  if (occ)
+    launch_trace_any(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), (int)n, occ, st);
+  else
+    launch_trace_closest(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), (int)n,
+                         (float4*)hit4, st);
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// ---------------------------------------------------------------- scene commit
+void SceneObj::commit() {
+  std::vector<std::shared_ptr<ScenePrim>> prims = slots;
+  gpu = build_gpu_scene(prims, YRT_STACK_DEPTH, static_cast<Device*>(dev)->gpu);
+}
+
+}  // namespace yrt
+
+// ====================================================================== C ABI
+using namespace yrt;
+
+struct YRTDevice_ {
+  Device* d;
+};
+
+#define DEV_GUARD(dev, failret)                                         \
+  if (!dev || !dev->d) return failret;                                  \
+  std::lock_guard<std::recursive_mutex> _lk(dev->d->mu);                \
+  try {
+#define DEV_END(failret)                                                \
+  }                                                                     \
+  catch (const std::exception& e) {                                     \
+    dev->d->lastError = e.what();                                       \
+    return failret;                                                     \
+  }
+
+extern "C" {
+
+YRTDevice yrtNewDevice(const char* parms, size_t, int, const char*) {
+  int devId = 0;
+  bool gpu = true;
+  if (parms && strncmp(parms, "device=", 7) == 0) devId = atoi(parms + 7);
+  if (parms && strcmp(parms, "host") == 0) gpu = false;
+  try {
+    auto* d = new YRTDevice_;
+    d->d = new Device(devId, gpu);
+    return d;
+  } catch (...) {
+    return nullptr;
+  }
+}
+
+void yrtDeleteDevice(YRTDevice dev) {
+  if (!dev) return;
+  delete dev->d;
+  delete dev;
+}
+
+const char* yrtGetLastError(YRTDevice dev) { return dev && dev->d ? dev->d->lastError.c_str() : "no device"; }
+
+static bool ieq(const char* a, const char* b) { return a && b && strcasecmp(a, b) == 0; }
+
+YRTHandle yrtNewCamera(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "pinhole") && !ieq(type, "stereo"))
+    throw std::runtime_error(std::string("camera type '") + type + "' is outside the MI355X device's scope");
+  return dev->d->wrap(std::make_shared<CameraObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewData(YRTDevice dev, const char* type, size_t bytes, const void* data) {
+  DEV_GUARD(dev, nullptr)
+  auto o = std::make_shared<DataObj>();
+  o->type = type ? type : "immutable";
+  o->bytes.assign((const uint8_t*)data, (const uint8_t*)data + bytes);
+  return dev->d->wrap(o);
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewImage(YRTDevice dev, const char* type, size_t width, size_t height, const void* data) {
+  DEV_GUARD(dev, nullptr)
+  auto o = std::make_shared<ImageObj>();
+  image_from_memory(type, (int)width, (int)height, data, *o);
+  return dev->d->wrap(o);
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewImageFromFile(YRTDevice dev, const char* file) {
+  DEV_GUARD(dev, nullptr)
+  auto o = std::make_shared<ImageObj>();
+  // SingleRayDevice::rtNewImageFromFile (singleray_device.cpp:238-251): failed load -> 1x1 white
+  if (!image_load(file, *o)) {
+    o->width = o->height = 1;
+    o->format = IMG_RGBA8;
+    o->data = {255, 255, 255, 255};
+  }
+  return dev->d->wrap(o);
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewTexture(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "bilinear") && !ieq(type, "nearest") && !ieq(type, "image"))
+    throw std::runtime_error(std::string("unsupported texture type: ") + type);
+  return dev->d->wrap(std::make_shared<TextureObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewMaterial(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  static const char* ok[] = {"Matte", "MatteTextured", "MetallicPaint", "Obj", "Uber", "ThinDielectric", "ThinGlass"};
+  bool found = false;
+  for (auto* n : ok) found |= ieq(type, n);
+  if (!found)
+    throw std::runtime_error(std::string("material type '") + type +
+                             "' is outside the MI355X device's scope (SURVEY.md §2 row 11)");
+  return dev->d->wrap(std::make_shared<MaterialObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewShape(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "trianglemesh") && !ieq(type, "sphere") && !ieq(type, "triangle"))
+    throw std::runtime_error(std::string("shape type '") + type + "' is outside the MI355X device's scope");
+  return dev->d->wrap(std::make_shared<ShapeObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewLight(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "ambientlight") && !ieq(type, "trianglelight") && !ieq(type, "hdrilight"))
+    throw std::runtime_error(std::string("light type '") + type +
+                             "' is outside the MI355X device's scope (SURVEY.md §2 row 13)");
+  return dev->d->wrap(std::make_shared<LightObj>(type));
+  DEV_END(nullptr)
+}
+
+static A3 xfm_or_identity(const float* t) {
+  if (!t) return a3_identity();
+  return a3(l3(v3(t[0], t[1], t[2]), v3(t[3], t[4], t[5]), v3(t[6], t[7], t[8])), v3(t[9], t[10], t[11]));
+}
+
+YRTHandle yrtNewShapePrimitive(YRTDevice dev, YRTHandle shape, YRTHandle material, const float* transform12,
+                               int faceCamera) {
+  DEV_GUARD(dev, nullptr)
+  auto p = std::make_shared<PrimitiveObj>();
+  p->shapeHandle = dev->d->get<ShapeObj>(shape, "shape");
+  p->materialHandle = dev->d->get<MaterialObj>(material, "material");
+  if (!p->shapeHandle) throw std::runtime_error("invalid shape handle");
+  p->transform = xfm_or_identity(transform12);
+  p->faceCamera = faceCamera != 0;
+  return dev->d->wrap(p);
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewLightPrimitive(YRTDevice dev, YRTHandle light, YRTHandle material, const float* transform12) {
+  DEV_GUARD(dev, nullptr)
+  auto p = std::make_shared<PrimitiveObj>();
+  p->lightHandle = dev->d->get<LightObj>(light, "light");
+  p->materialHandle = dev->d->get<MaterialObj>(material, "material");
+  if (!p->lightHandle) throw std::runtime_error("invalid light handle");
+  p->transform = xfm_or_identity(transform12);
+  return dev->d->wrap(p);
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewScene(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  return dev->d->wrap(std::make_shared<SceneObj>(type ? type : "default"));
+  DEV_END(nullptr)
+}
+
+// BackendSceneFlat::Handle::setPrimitive (api/scene_flat.h:48-58)
+int yrtSetPrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim) {
+  DEV_GUARD(dev, -1)
+  auto s = dev->d->get<SceneObj>(scene, "scene");
+  auto p = dev->d->get<PrimitiveObj>(prim, "primitive");
+  if (!s || !p) throw std::runtime_error("invalid scene or primitive");
+  if (slot >= s->slots.size()) s->slots.resize(slot + 1);
+  auto sp = std::make_shared<ScenePrim>();
+  std::shared_ptr<const MeshInst> shape;
+  std::shared_ptr<const LightInst> light;
+  if (p->shapeHandle) {
+    if (!p->shapeHandle->inst) throw std::runtime_error("shape not committed");
+    shape = p->shapeHandle->inst;
+  }
+  if (p->lightHandle) {
+    if (!p->lightHandle->inst) throw std::runtime_error("light not committed");
+    light = p->lightHandle->inst;
+    shape = light->shape;
+  }
+  if (shape) sp->shape = shape->transform(p->transform);
+  if (light) sp->light = light->transform(p->transform, p->illumMask, p->shadowMask);
+  if (p->materialHandle) {
+    if (!p->materialHandle->inst) throw std::runtime_error("material not committed");
+    sp->material = p->materialHandle->inst;
+  }
+  sp->illumMask = p->illumMask;
+  sp->shadowMask = p->shadowMask;
+  sp->faceCamera = p->faceCamera;
+  sp->prim = p;
+  s->slots[slot] = sp;
+  return 0;
+  DEV_END(-1)
+}
+
+YRTHandle yrtNewToneMapper(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "default")) throw std::runtime_error(std::string("unknown tonemapper: ") + type);
+  return dev->d->wrap(std::make_shared<ToneMapperObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewRenderer(YRTDevice dev, const char* type) {
+  DEV_GUARD(dev, nullptr)
+  if (!ieq(type, "pathtracer") && !ieq(type, "pt") && !ieq(type, "debug") && !ieq(type, "integrator"))
+    throw std::runtime_error(std::string("unknown renderer: ") + type);
+  return dev->d->wrap(std::make_shared<RendererObj>(type));
+  DEV_END(nullptr)
+}
+
+YRTHandle yrtNewFrameBuffer(YRTDevice dev, const char* type, size_t width, size_t height, size_t buffers, void** ptrs) {
+  DEV_GUARD(dev, nullptr)
+  auto f = std::make_shared<FrameBufferObj>(type);
+  if (ieq(type, "RGB8")) { f->format = FB_RGB8; f->stride = (3 * width + 3) / 4 * 4; }
+  else if (ieq(type, "RGBA8")) { f->format = FB_RGBA8; f->stride = 4 * width; }
+  else if (ieq(type, "RGB_FLOAT32")) { f->format = FB_RGB_FLOAT32; f->stride = 12 * width; }
+  else if (ieq(type, "RGBA_FLOAT32")) { f->format = FB_RGBA_FLOAT32; f->stride = 16 * width; }
+  else throw std::runtime_error(std::string("unknown framebuffer format: ") + type);
+  f->width = (int)width;
+  f->height = (int)height;
+  f->depth = (int)std::max<size_t>(1, buffers);
+  if (ptrs) f->userPtrs.assign(ptrs, ptrs + f->depth);
+  else
+    for (int i = 0; i < f->depth; ++i) f->host.emplace_back(f->stride * height, 0);
+  return dev->d->wrap(f);
+  DEV_END(nullptr)
+}
+
+int yrtIncRef(YRTDevice dev, YRTHandle h) {
+  DEV_GUARD(dev, -1)
+  dev->d->ref(h)->refs++;
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtDecRef(YRTDevice dev, YRTHandle h) {
+  DEV_GUARD(dev, -1)
+  HandleRef* r = dev->d->ref(h);
+  if (--r->refs == 0) {
+    dev->d->handles.erase(r);
+    delete r;
+  }
+  return 0;
+  DEV_END(-1)
+}
+
+static int set_variant(YRTDevice dev, YRTHandle h, const char* prop, const Variant& v) {
+  DEV_GUARD(dev, -1)
+  if (!prop) throw std::runtime_error("invalid property");
+  dev->d->ref(h)->obj->parms.set(prop, v);
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtSetBool1(YRTDevice dev, YRTHandle h, const char* p, int x) {
+  Variant v; v.type = Variant::BOOL1; v.i[0] = x != 0;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetInt1(YRTDevice dev, YRTHandle h, const char* p, int x) {
+  Variant v; v.type = Variant::INT1; v.i[0] = x;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetInt2(YRTDevice dev, YRTHandle h, const char* p, int x, int y) {
+  Variant v; v.type = Variant::INT2; v.i[0] = x; v.i[1] = y;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetInt3(YRTDevice dev, YRTHandle h, const char* p, int x, int y, int z) {
+  Variant v; v.type = Variant::INT3; v.i[0] = x; v.i[1] = y; v.i[2] = z;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetInt4(YRTDevice dev, YRTHandle h, const char* p, int x, int y, int z, int w) {
+  Variant v; v.type = Variant::INT4; v.i[0] = x; v.i[1] = y; v.i[2] = z; v.i[3] = w;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetFloat1(YRTDevice dev, YRTHandle h, const char* p, float x) {
+  Variant v; v.type = Variant::FLOAT1; v.f[0] = x;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetFloat2(YRTDevice dev, YRTHandle h, const char* p, float x, float y) {
+  Variant v; v.type = Variant::FLOAT2; v.f[0] = x; v.f[1] = y;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetFloat3(YRTDevice dev, YRTHandle h, const char* p, float x, float y, float z) {
+  Variant v; v.type = Variant::FLOAT3; v.f[0] = x; v.f[1] = y; v.f[2] = z;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetFloat4(YRTDevice dev, YRTHandle h, const char* p, float x, float y, float z, float w) {
+  Variant v; v.type = Variant::FLOAT4; v.f[0] = x; v.f[1] = y; v.f[2] = z; v.f[3] = w;
+  return set_variant(dev, h, p, v);
+}
+int yrtGetFloat3(YRTDevice dev, YRTHandle h, const char* p, float* x, float* y, float* z) {
+  DEV_GUARD(dev, -1)
+  const Variant* v = dev->d->ref(h)->obj->parms.find(p);
+  if (!v || v->type != Variant::FLOAT3) throw std::runtime_error(std::string("no float3 property ") + p);
+  *x = v->f[0]; *y = v->f[1]; *z = v->f[2];
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetArray(YRTDevice dev, YRTHandle h, const char* p, const char* type, YRTHandle data, size_t size,
+                size_t stride, size_t ofs) {
+  DEV_GUARD(dev, -1)
+  auto d = dev->d->get<DataObj>(data, "data");
+  if (!d) throw std::runtime_error("invalid data handle");
+  Variant v;
+  v.type = Variant::DATA;
+  v.obj = d;
+  v.dataType = type;
+  v.size = size;
+  size_t es = 0;
+  if (ieq(type, "float2")) es = 8;
+  else if (ieq(type, "float3") || ieq(type, "int3")) es = 12;
+  else if (ieq(type, "float4") || ieq(type, "int4")) es = 16;
+  else if (ieq(type, "float1") || ieq(type, "int1")) es = 4;
+  else if (ieq(type, "int2")) es = 8;
+  else throw std::runtime_error(std::string("unknown array type: ") + type);
+  v.stride = stride == (size_t)-1 ? es : stride;
+  v.ofs = ofs;
+  if (size && v.ofs + (size - 1) * v.stride + es > d->bytes.size()) throw std::runtime_error("array exceeds data");
+  dev->d->ref(h)->obj->parms.set(p, v);
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetString(YRTDevice dev, YRTHandle h, const char* p, const char* str) {
+  Variant v; v.type = Variant::STRING; v.str = str ? str : "";
+  return set_variant(dev, h, p, v);
+}
+int yrtSetImage(YRTDevice dev, YRTHandle h, const char* p, YRTHandle image) {
+  DEV_GUARD(dev, -1)
+  Variant v;
+  v.type = Variant::IMAGE;
+  v.obj = dev->d->get<ImageObj>(image, "image");
+  dev->d->ref(h)->obj->parms.set(p, v);
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetTexture(YRTDevice dev, YRTHandle h, const char* p, YRTHandle texture) {
+  DEV_GUARD(dev, -1)
+  Variant v;
+  v.type = Variant::TEXTURE;
+  v.obj = dev->d->get<TextureObj>(texture, "texture");
+  dev->d->ref(h)->obj->parms.set(p, v);
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetTransform(YRTDevice dev, YRTHandle h, const char* p, const float* t) {
+  Variant v;
+  v.type = Variant::TRANSFORM;
+  for (int i = 0; i < 12; ++i) v.f[i] = t[i];
+  return set_variant(dev, h, p, v);
+}
+int yrtSetPointer(YRTDevice dev, YRTHandle h, const char* p, void* ptr) {
+  Variant v; v.type = Variant::POINTER; v.ptr = ptr;
+  return set_variant(dev, h, p, v);
+}
+int yrtClear(YRTDevice dev, YRTHandle h) {
+  DEV_GUARD(dev, -1)
+  dev->d->ref(h)->obj->parms.clear();
+  return 0;
+  DEV_END(-1)
+}
+int yrtCommit(YRTDevice dev, YRTHandle h) {
+  DEV_GUARD(dev, -1)
+  if (dev->d->gpu) HIP_CHECK(hipSetDevice(dev->d->hipDevice));
+  dev->d->ref(h)->obj->commit();
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene, YRTHandle tonemapper,
+                   YRTHandle framebuffer, int accumulate) {
+  DEV_GUARD(dev, -1)
+  auto R = dev->d->get<RendererObj>(renderer, "renderer");
+  auto C = dev->d->get<CameraObj>(camera, "camera");
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  auto T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
+  auto F = dev->d->get<FrameBufferObj>(framebuffer, "framebuffer");
+  if (!R || !C || !S || !T || !F) throw std::runtime_error("rtRenderFrame: null handle");
+  if (!dev->d->gpu) throw std::runtime_error("rtRenderFrame: host-only device (created with parms \"host\")");
+  dev->d->render(*R, *C, *S, *T, *F, accumulate);
+  return 0;
+  DEV_END(-1)
+}
+
+void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle fb, int bufID) {
+  DEV_GUARD(dev, nullptr)
+  auto F = dev->d->get<FrameBufferObj>(fb, "framebuffer");
+  const int id = bufID < 0 ? F->cur : bufID;
+  return F->buffer(id);
+  DEV_END(nullptr)
+}
+int yrtUnmapFrameBuffer(YRTDevice dev, YRTHandle fb, int) {
+  DEV_GUARD(dev, -1)
+  (void)dev->d->get<FrameBufferObj>(fb, "framebuffer");
+  return 0;
+  DEV_END(-1)
+}
+int yrtSwapBuffers(YRTDevice dev, YRTHandle fb) {
+  DEV_GUARD(dev, -1)
+  auto F = dev->d->get<FrameBufferObj>(fb, "framebuffer");
+  F->cur = (F->cur + 1) % F->depth;
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetStatusCallback(YRTDevice dev, YRTHandle renderer, YRTStatusCallback cb, void* user) {
+  DEV_GUARD(dev, -1)
+  auto R = dev->d->get<RendererObj>(renderer, "renderer");
+  R->statusCallback = (void*)cb;
+  R->statusUser = user;
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetStopFlag(YRTDevice dev, YRTHandle renderer, volatile int* flag) {
+  DEV_GUARD(dev, -1)
+  auto R = dev->d->get<RendererObj>(renderer, "renderer");
+  R->stopFlag = (std::atomic<bool>*)flag;  // polled as a byte-sized bool between batches
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtIntersect(YRTDevice dev, YRTHandle scene, const float* org4, const float* dir4, uint32_t n, float* hit4,
+                 void* stream) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  dev->d->intersect(*S, org4, dir4, n, hit4, nullptr, stream ? (hipStream_t)stream : dev->d->stream);
+  return 0;
+  DEV_END(-1)
+}
+int yrtOccluded(YRTDevice dev, YRTHandle scene, const float* org4, const float* dir4, uint32_t n, int32_t* occ,
+                void* stream) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  dev->d->intersect(*S, org4, dir4, n, nullptr, occ, stream ? (hipStream_t)stream : dev->d->stream);
+  return 0;
+  DEV_END(-1)
+}
+int yrtTriangleIds(YRTDevice dev, YRTHandle scene, int32_t tri, int32_t* geomID, int32_t* primID) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!S->gpu) throw std::runtime_error("scene not committed");
+  if (tri < 0 || tri >= S->gpu->numTris) { *geomID = -1; *primID = -1; return 0; }
+  const int g = S->gpu->hTriGeom[tri];
+  *geomID = g;
+  *primID = tri - S->gpu->hGeoms[g].triBase;
+  return 0;
+  DEV_END(-1)
+}
+int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out) {
+  DEV_GUARD(dev, -1)
+  *out = dev->d->stats;
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetKernelTiming(YRTDevice dev, int enable) {
+  DEV_GUARD(dev, -1)
+  dev->d->kernelTiming = enable != 0;
+  return 0;
+  DEV_END(-1)
+}
+int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!S->gpu) throw std::runtime_error("scene not committed");
+  out->numTriangles = S->gpu->numTris;
+  out->numGeometries = S->gpu->numGeoms;
+  out->numNodes = (int64_t)S->gpu->hNodes.size();
+  out->bvhDepth = S->gpu->bvhDepth;
+  out->numLights = S->gpu->view.numLights;
+  out->buildSeconds = S->gpu->buildSeconds;
+  for (int k = 0; k < 3; ++k) { out->bboxLo[k] = S->gpu->bboxLo[k]; out->bboxHi[k] = S->gpu->bboxHi[k]; }
+  return 0;
+  DEV_END(-1)
+}
+int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes, void* tris, size_t trisBytes) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!S->gpu) throw std::runtime_error("scene not committed");
+  const size_t nb = S->gpu->hNodes.size() * sizeof(GpuNode), tb = S->gpu->hTris.size() * sizeof(GpuTri);
+  if (nodesBytes < nb || trisBytes < tb) throw std::runtime_error("buffers too small");
+  memcpy(nodes, S->gpu->hNodes.data(), nb);
+  memcpy(tris, S->gpu->hTris.data(), tb);
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetFrameSeed(YRTDevice dev, uint32_t seed) {
+  DEV_GUARD(dev, -1)
+  dev->d->frameSeed = seed;
+  return 0;
+  DEV_END(-1)
+}
+int yrtSetBatchCapacity(YRTDevice dev, int64_t paths) {
+  DEV_GUARD(dev, -1)
+  if (paths < 256) throw std::runtime_error("capacity must be >= 256 paths");
+  dev->d->capacity = paths;
+  return 0;
+  DEV_END(-1)
+}
+int64_t yrt_export_frame_impl(const Object* renderer, const Object* camera, const SceneObj* scene, uint32_t frameSeed,
+                              void* buf, size_t bytes);
+int64_t yrtExportFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene, void* buf, size_t bytes) {
+  DEV_GUARD(dev, -1)
+  auto R = dev->d->get<RendererObj>(renderer, "renderer");
+  auto C = dev->d->get<CameraObj>(camera, "camera");
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!R || !C || !S) throw std::runtime_error("yrtExportFrame: null handle");
+  return yrt_export_frame_impl(R.get(), C.get(), S.get(), dev->d->frameSeed, buf, bytes);
+  DEV_END(-1)
+}
+
+int yrtDebugSampleTable(int spp, int sets, int iteration, int num1D, int num2D, const char* filter, float* out,
+                        size_t outFloats) {
+  try {
+    SampleRequest req;
+    req.spp = spp;
+    req.sets = sets;
+    req.iteration = iteration;
+    req.num1D = num1D;
+    req.num2D = num2D;
+    req.filter = filter ? filter : "bspline";
+    SampleTable t;
+    build_sample_table(req, t);
+    if (out && outFloats >= t.dims.size()) memcpy(out, t.dims.data(), t.dims.size() * sizeof(float));
+    return t.numRecords;
+  } catch (...) {
+    return -1;
+  }
+}
+
+int yrtSetTileShard(YRTDevice dev, int index, int count) {
+  DEV_GUARD(dev, -1)
+  if (count < 1 || index < 0 || index >= count) throw std::runtime_error("invalid shard");
+  dev->d->shardIndex = index;
+  dev->d->shardCount = count;
+  return 0;
+  DEV_END(-1)
+}
+
+}  // extern "C"

@@ -1,0 +1,245 @@
+// scene_gpu.cpp — flatten a committed scene into HBM buffers + BVH.
+//
+// Follows BackendSceneFlat::Handle::create (api/scene_flat.h:72-97) and the
+// BackendSceneFlat ctor (:105-121): geomID = index among primitives that have a shape, in
+// slot order; allLights in slot order; envLights = ambient/HDRI lights. Geometry is the
+// world-space result of Shape::transform, exactly what extract() handed to Embree.
+#include "scene_gpu.h"
+
+#include <string.h>
+
+#include <chrono>
+#include <map>
+
+#include "bvh_build.h"
+#include "distribution.h"
+
+namespace yrt {
+
+std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<ScenePrim>>& prims, int stackDepth,
+                                          bool upload) {
+  auto t0 = std::chrono::steady_clock::now();
+  auto S = std::make_shared<GpuScene>();
+  if (upload) HIP_CHECK(hipGetDevice(&S->device));
+
+  std::vector<float4> positions, normals;
+  std::vector<float2> texcoords;
+  std::vector<int4> indices;
+  std::vector<int> triGeom;
+  std::vector<float> triVerts;
+  std::vector<uint32_t> triFlags;
+  std::vector<GpuGeom> geoms;
+  std::vector<GpuMaterial> materials;
+  std::vector<GpuTexture> textures;
+  std::vector<GpuImage> images;
+  std::vector<uint8_t> texels;
+  std::vector<GpuLight> lights;
+  std::vector<int> envLights;
+  std::map<const MaterialInst*, int> matIds;
+  std::map<const TextureInst*, int> texIds;
+  std::map<const ImageObj*, int> imgIds;
+
+  auto imageId = [&](const std::shared_ptr<ImageObj>& im) -> int {
+    auto it = imgIds.find(im.get());
+    if (it != imgIds.end()) return it->second;
+    GpuImage g;
+    memset(&g, 0, sizeof(g));
+    g.width = im->width;
+    g.height = im->height;
+    g.format = im->format;
+    size_t off = (texels.size() + 15) & ~size_t(15);
+    texels.resize(off);
+    g.offset = (int64_t)off;
+    texels.insert(texels.end(), im->data.begin(), im->data.end());
+    images.push_back(g);
+    return imgIds[im.get()] = (int)images.size() - 1;
+  };
+  auto textureId = [&](const std::shared_ptr<const TextureInst>& t) -> int {
+    if (!t) return -1;
+    auto it = texIds.find(t.get());
+    if (it != texIds.end()) return it->second;
+    GpuTexture g;
+    memset(&g, 0, sizeof(g));
+    g.image = imageId(t->image);
+    g.filter = t->filter;
+    g.invert = t->invert ? 1 : 0;
+    textures.push_back(g);
+    return texIds[t.get()] = (int)textures.size() - 1;
+  };
+  auto materialId = [&](const std::shared_ptr<const MaterialInst>& m) -> int {
+    if (!m) return -1;
+    auto it = matIds.find(m.get());
+    if (it != matIds.end()) return it->second;
+    GpuMaterial g = m->gm;
+    for (int k = 0; k < 5; ++k) g.tex[k] = textureId(m->tex[k]);
+    materials.push_back(g);
+    return matIds[m.get()] = (int)materials.size() - 1;
+  };
+
+  // lights first (allLights in slot order) so geometries can reference their area light
+  std::vector<int> primLight(prims.size(), -1);
+  int numPrecomp = 0;
+  for (size_t i = 0; i < prims.size(); ++i) {
+    const auto& p = prims[i];
+    if (!p || !p->light) continue;
+    const LightInst& L = *p->light;
+    GpuLight g;
+    memset(&g, 0, sizeof(g));
+    g.type = L.type;
+    g.illumMask = L.illumMask;
+    g.shadowMask = L.shadowMask;
+    g.precomputed = -1;
+    g.L[0] = L.L.x; g.L[1] = L.L.y; g.L[2] = L.L.z;
+    auto st3 = [](float* d, V3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
+    st3(g.v0, L.v0); st3(g.v1, L.v1); st3(g.v2, L.v2);
+    st3(g.e1, L.e1); st3(g.e2, L.e2); st3(g.Ng, L.Ng);
+    auto stA = [](float* d, const A3& a) {
+      const float v[12] = {a.l.vx.x, a.l.vx.y, a.l.vx.z, a.l.vy.x, a.l.vy.y, a.l.vy.z,
+                           a.l.vz.x, a.l.vz.y, a.l.vz.z, a.p.x,    a.p.y,    a.p.z};
+      memcpy(d, v, sizeof(v));
+    };
+    stA(g.l2w, L.l2w);
+    stA(g.w2l, L.w2l);
+    if (L.type == LIGHT_AMBIENT || L.type == LIGHT_HDRI) {
+      g.isEnv = 1;
+      envLights.push_back((int)lights.size());
+    }
+    if (L.type == LIGHT_HDRI) {
+      g.image = imageId(L.image);
+      g.hdriW = L.image->width;
+      g.hdriH = L.image->height;
+    }
+    if (L.precompute()) {
+      g.precomputed = numPrecomp++;
+      // HDRILight::sample (lights/hdrilight.cpp:77-87), evaluated once per sample record
+      auto lp = p->light;
+      LightSampleSource src;
+      src.baseSample = 0;  // lightSampleID: first request2D() (pathtraceintegrator.cpp:39)
+      src.sample = [lp](float ux, float uy, float* o) {
+        const int w = lp->image->width, h = lp->image->height;
+        float sx, sy, pdf;
+        dist2d_sample(lp->ycdf, lp->ypdf, lp->xcdf, lp->xpdf, w, h, ux, uy, sx, sy, pdf);
+        const float theta = kPi * sy * rcpf_(float(h));
+        const float phi = kTwoPi * (1.0f - sx * rcpf_(float(w)));
+        const V3 _wi = v3(-sinf(theta) * cosf(phi), cosf(theta), -sinf(theta) * sinf(phi));
+        const V3 wi = xfmVector(lp->l2w, _wi);
+        const float wpdf = pdf * rcpf_(kTwoPi * kPi * sinf(theta));
+        float c[4];
+        lp->image->get(std::max(0, std::min((int)sx, w - 1)), std::max(0, std::min((int)sy, h - 1)), c);
+        o[0] = wi.x; o[1] = wi.y; o[2] = wi.z; o[3] = wpdf;
+        o[4] = lp->L.x * c[0]; o[5] = lp->L.y * c[1]; o[6] = lp->L.z * c[2];
+        o[7] = INFINITY;
+      };
+      S->precomputed.push_back(src);
+    }
+    primLight[i] = (int)lights.size();
+    lights.push_back(g);
+    S->allLights.push_back(p->light);
+  }
+
+  // geometries in slot order (geomID = compacted index)
+  int gidBase = 0;
+  for (size_t i = 0; i < prims.size(); ++i) {
+    const auto& p = prims[i];
+    if (!p || !p->shape) continue;
+    const MeshInst& m = *p->shape;
+    GpuGeom g;
+    memset(&g, 0, sizeof(g));
+    g.kind = m.kind;
+    g.material = materialId(p->material);
+    g.light = primLight[i];
+    g.illumMask = p->illumMask;
+    g.shadowMask = p->shadowMask;
+    g.vtxBase = (int)positions.size();
+    g.triBase = gidBase;
+    g.flags = (m.nor.empty() ? 0 : GF_NORMALS) | (m.uv.empty() ? 0 : GF_TEXCOORDS) | (m.cull ? GF_CULL : 0);
+    g.Ng[0] = m.Ng.x; g.Ng[1] = m.Ng.y; g.Ng[2] = m.Ng.z;
+    const int geomId = (int)geoms.size();
+    for (size_t k = 0; k < m.pos.size(); ++k) {
+      positions.push_back(make_float4(m.pos[k].x, m.pos[k].y, m.pos[k].z, 0.f));
+      if (!m.nor.empty()) normals.push_back(make_float4(m.nor[k].x, m.nor[k].y, m.nor[k].z, 0.f));
+      else normals.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+      if (!m.uv.empty()) texcoords.push_back(make_float2(m.uv[2 * k], m.uv[2 * k + 1]));
+      else texcoords.push_back(make_float2(0.f, 0.f));
+    }
+    const int nt = (int)(m.tri.size() / 3);
+    for (int t = 0; t < nt; ++t) {
+      const int a = m.tri[3 * t], b = m.tri[3 * t + 1], c = m.tri[3 * t + 2];
+      indices.push_back(make_int4(g.vtxBase + a, g.vtxBase + b, g.vtxBase + c, geomId));
+      triGeom.push_back(geomId);
+      const V3 va = m.pos[a], vb = m.pos[b], vc = m.pos[c];
+      const float tv[9] = {va.x, va.y, va.z, vb.x, vb.y, vb.z, vc.x, vc.y, vc.z};
+      triVerts.insert(triVerts.end(), tv, tv + 9);
+      triFlags.push_back(m.cull ? 1u : 0u);
+    }
+    gidBase += nt;
+    geoms.push_back(g);
+  }
+  if (gidBase >= (1 << 26)) throw std::runtime_error("scene exceeds 2^26 triangles (stack entry packing)");
+
+  BvhResult bvh;
+  build_bvh(triVerts, triFlags, stackDepth, bvh);
+  S->bvhDepth = bvh.maxDepth;
+  S->numTris = gidBase;
+  S->numGeoms = (int)geoms.size();
+  for (int k = 0; k < 3; ++k) { S->bboxLo[k] = INFINITY; S->bboxHi[k] = -INFINITY; }
+  for (size_t i = 0; i < triVerts.size(); i += 3)
+    for (int k = 0; k < 3; ++k) {
+      S->bboxLo[k] = std::min(S->bboxLo[k], triVerts[i + k]);
+      S->bboxHi[k] = std::max(S->bboxHi[k], triVerts[i + k]);
+    }
+
+  if (!upload) {
+    S->hNodes = std::move(bvh.nodes);
+    S->hTris = std::move(bvh.tris);
+    S->hGeoms = geoms;
+    S->hTriGeom = triGeom;
+    S->view.numLights = (int)lights.size();
+    S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return S;
+  }
+  S->nodes.upload(bvh.nodes);
+  S->tris.upload(bvh.tris);
+  S->triGeom.upload(triGeom);
+  S->indices.upload(indices);
+  S->positions.upload(positions);
+  S->normals.upload(normals);
+  S->texcoords.upload(texcoords);
+  S->geoms.upload(geoms);
+  S->materials.upload(materials);
+  S->textures.upload(textures);
+  S->images.upload(images);
+  S->texels.upload(texels);
+  S->lights.upload(lights);
+  S->envLights.upload(envLights);
+
+  SceneView& v = S->view;
+  v.nodes = S->nodes.as<GpuNode>();
+  v.tris = S->tris.as<GpuTri>();
+  v.triGeom = S->triGeom.as<int>();
+  v.indices = S->indices.as<int4>();
+  v.positions = S->positions.as<float4>();
+  v.normals = S->normals.as<float4>();
+  v.texcoords = S->texcoords.as<float2>();
+  v.geoms = S->geoms.as<GpuGeom>();
+  v.materials = S->materials.as<GpuMaterial>();
+  v.textures = S->textures.as<GpuTexture>();
+  v.images = S->images.as<GpuImage>();
+  v.texels = S->texels.as<uint8_t>();
+  v.lights = S->lights.as<GpuLight>();
+  v.envLights = S->envLights.as<int>();
+  v.hdriDist = nullptr;
+  v.numLights = (int)lights.size();
+  v.numEnvLights = (int)envLights.size();
+  v.numNodes = (int)bvh.nodes.size();
+  v.numTris = gidBase;
+
+  S->hNodes = std::move(bvh.nodes);
+  S->hTris = std::move(bvh.tris);
+  S->hGeoms = geoms;
+  S->hTriGeom = triGeom;
+  S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return S;
+}
+
+}  // namespace yrt

@@ -1,0 +1,73 @@
+// scene_gpu.h — a committed scene flattened into HBM (layout: common/yrt_gpu_types.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../kernels/yrt_kernels.h"
+#include "objects.h"
+#include "sampler.h"
+
+namespace yrt {
+
+#define HIP_CHECK(x)                                                                              \
+  do {                                                                                            \
+    hipError_t _e = (x);                                                                          \
+    if (_e != hipSuccess)                                                                         \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " #x);    \
+  } while (0)
+
+// RAII device allocation
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() {}
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void alloc(size_t n) {
+    if (n <= bytes && p) return;
+    release();
+    if (n == 0) n = 16;
+    HIP_CHECK(hipMalloc(&p, n));
+    bytes = n;
+  }
+  template <class T>
+  void upload(const std::vector<T>& v) {
+    alloc(v.size() * sizeof(T));
+    if (!v.empty()) HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct GpuScene {
+  int device = 0;
+  DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels,
+      lights, envLights, hdriDist;
+  SceneView view{};
+  // host mirrors (BVH export, precomputed light sampling, stats)
+  std::vector<GpuNode> hNodes;
+  std::vector<GpuTri> hTris;
+  std::vector<GpuGeom> hGeoms;
+  std::vector<int> hTriGeom;
+  std::vector<std::shared_ptr<const LightInst>> allLights;
+  std::vector<LightSampleSource> precomputed;   // LightSampleSource per precompute() light
+  int numTris = 0, numGeoms = 0, bvhDepth = 0;
+  double buildSeconds = 0;
+  float bboxLo[3] = {0, 0, 0}, bboxHi[3] = {0, 0, 0};
+};
+
+std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<ScenePrim>>& prims, int stackDepth,
+                                          bool upload);
+
+}  // namespace yrt

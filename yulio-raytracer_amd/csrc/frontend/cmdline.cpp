@@ -1,0 +1,468 @@
+// cmdline.cpp — the renderer's command line / .ecs parser and output mode.
+//
+//   createGlobalObjects        devices/renderer/renderer.cpp:352-369
+//   parsePathTracer            :414-442        parseDebugRenderer :393-412
+//   parseCommandLine           :974-1403
+//   createCamera / createScene :309-345
+//   outputMode                 :508-905 (mono and non-FPR stereo branches)
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+#include "frontend.h"
+
+namespace yrtfe {
+
+yrt_affine look_at(yrt_v3 eye, yrt_v3 point, yrt_v3 up) {
+  auto sub = [](yrt_v3 a, yrt_v3 b) { return yrt_v3{a.x - b.x, a.y - b.y, a.z - b.z}; };
+  auto cross = [](yrt_v3 a, yrt_v3 b) {
+    return yrt_v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+  };
+  auto norm = [](yrt_v3 a) {
+    const float r = 1.0f / sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    return yrt_v3{a.x * r, a.y * r, a.z * r};
+  };
+  const yrt_v3 Z = norm(sub(point, eye));
+  const yrt_v3 U = norm(cross(up, Z));
+  const yrt_v3 V = norm(cross(Z, U));
+  yrt_affine a = {{U.x, U.y, U.z, V.x, V.y, V.z, Z.x, Z.y, Z.z, eye.x, eye.y, eye.z}};
+  return a;
+}
+
+std::vector<std::string> tokenize_args(int argc, const char** argv) {
+  std::vector<std::string> t;
+  for (int i = 0; i < argc; ++i) t.push_back(argv[i]);
+  return t;
+}
+
+// ParseStream over LineCommentFilter(file, "#") (common/lexers)
+static std::vector<std::string> tokenize_file(const std::string& file) {
+  std::ifstream in(file);
+  if (!in) throw std::runtime_error("cannot open file " + file);
+  std::vector<std::string> out;
+  std::string line;
+  while (std::getline(in, line)) {
+    const size_t h = line.find('#');
+    if (h != std::string::npos) line = line.substr(0, h);
+    std::string cur;
+    for (char c : line) {
+      if (c == ' ' || c == '\t' || c == '\r' || c == '\n') {
+        if (!cur.empty()) out.push_back(cur), cur.clear();
+      } else if (c == '{' || c == '}' || c == '=') {
+        if (!cur.empty()) out.push_back(cur), cur.clear();
+        out.push_back(std::string(1, c));
+      } else {
+        cur += c;
+      }
+    }
+    if (!cur.empty()) out.push_back(cur);
+  }
+  return out;
+}
+
+void RtState::createGlobalObjects() {
+  renderer = checkH(dev, yrtNewRenderer(dev, "pathtracer"), "rtNewRenderer");
+  if (depth >= 0) check(dev, yrtSetInt1(dev, renderer, "maxDepth", depth), "rtSetInt1");
+  check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowRay", tMaxShadowRay), "rtSetFloat1");
+  check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowJitter", tMaxShadowJitter), "rtSetFloat1");
+  check(dev, yrtSetFloat3(dev, renderer, "up", camUp.x, camUp.y, camUp.z), "rtSetFloat3");
+  check(dev, yrtSetInt1(dev, renderer, "sampler.spp", spp), "rtSetInt1");
+  check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+  tonemapper = checkH(dev, yrtNewToneMapper(dev, "default"), "rtNewToneMapper");
+  check(dev, yrtSetFloat1(dev, tonemapper, "gamma", gamma), "rtSetFloat1");
+  check(dev, yrtSetBool1(dev, tonemapper, "vignetting", vignetting), "rtSetBool1");
+  check(dev, yrtCommit(dev, tonemapper), "rtCommit(tonemapper)");
+  frameBuffer = checkH(dev, yrtNewFrameBuffer(dev, format.c_str(), width, height, numBuffers, nullptr), "rtNewFrameBuffer");
+}
+
+struct Stream {
+  const std::vector<std::string>& t;
+  size_t i = 0;
+  explicit Stream(const std::vector<std::string>& tk) : t(tk) {}
+  std::string peek() const { return i < t.size() ? t[i] : ""; }
+  std::string get() { return i < t.size() ? t[i++] : ""; }
+  void drop() { i++; }
+  float getFloat() {
+    const std::string s = get();
+    if (s.empty()) throw std::runtime_error("number expected");
+    return (float)atof(s.c_str());
+  }
+  int getInt() {
+    const std::string s = get();
+    if (s.empty()) throw std::runtime_error("integer expected");
+    return atoi(s.c_str());
+  }
+  yrt_v3 getV3() {
+    float x = getFloat(), y = getFloat(), z = getFloat();
+    return {x, y, z};
+  }
+  void force(const char* s) {
+    if (get() != s) throw std::runtime_error(std::string("token '") + s + "' expected");
+  }
+};
+
+void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std::string& path) {
+  Stream cin(tokens);
+  auto newRendererPathTracer = [&](const char* type) {
+    renderer = checkH(dev, yrtNewRenderer(dev, type), "rtNewRenderer");
+    if (depth >= 0) check(dev, yrtSetInt1(dev, renderer, "maxDepth", depth), "rtSetInt1");
+    if (strcmp(type, "debug") != 0)
+      check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowRay", tMaxShadowRay), "rtSetFloat1");
+    check(dev, yrtSetInt1(dev, renderer, "sampler.spp", spp), "rtSetInt1");
+    if (stopFlag) check(dev, yrtSetStopFlag(dev, renderer, (volatile int*)stopFlag), "stopFlag");
+    if (statusCallback)
+      check(dev, yrtSetStatusCallback(dev, renderer, (YRTStatusCallback)statusCallback, statusUser), "statusCallback");
+  };
+  auto addLight = [&](YRTHandle l) {
+    check(dev, yrtCommit(dev, l), "rtCommit(light)");
+    prims.push_back(checkH(dev, yrtNewLightPrimitive(dev, l, nullptr, nullptr), "rtNewLightPrimitive"));
+  };
+  while (true) {
+    const std::string tag = cin.get();
+    if (tag == "") return;
+    if (tag == "-c") {
+      const std::string file = join_path(path, cin.get());
+      parseCommandLine(tokenize_file(file), path_of(file));
+    } else if (tag == "--no-logging" || tag == "-profiling") {
+    } else if (tag == "-debug") {
+      debugging = true;
+    } else if (tag == "-i") {
+      const std::string file = join_path(path, cin.get());
+      auto p = loader->loadScene(file);
+      prims.insert(prims.end(), p.begin(), p.end());
+    } else if (tag == "-trisphere") {
+      YRTHandle s = checkH(dev, yrtNewShape(dev, "sphere"), "rtNewShape");
+      const yrt_v3 P = cin.getV3();
+      check(dev, yrtSetFloat3(dev, s, "P", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat1(dev, s, "r", cin.getFloat()), "rtSetFloat1");
+      check(dev, yrtSetInt1(dev, s, "numTheta", cin.getInt()), "rtSetInt1");
+      check(dev, yrtSetInt1(dev, s, "numPhi", cin.getInt()), "rtSetInt1");
+      check(dev, yrtCommit(dev, s), "rtCommit(shape)");
+      YRTHandle m = checkH(dev, yrtNewMaterial(dev, "matte"), "rtNewMaterial");
+      check(dev, yrtSetFloat3(dev, m, "reflection", 1.0f, 0.0f, 0.0f), "rtSetFloat3");
+      check(dev, yrtCommit(dev, m), "rtCommit(material)");
+      prims.push_back(checkH(dev, yrtNewShapePrimitive(dev, s, m, nullptr, 0), "rtNewShapePrimitive"));
+    } else if (tag == "-ambientlight") {
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "ambientlight"), "rtNewLight");
+      const yrt_v3 L = cin.getV3();
+      check(dev, yrtSetFloat3(dev, l, "L", L.x, L.y, L.z), "rtSetFloat3");
+      addLight(l);
+    } else if (tag == "-pointlight" || tag == "-masked_pointlight" || tag == "-directionallight" ||
+               tag == "-dirlight" || tag == "-distantlight" || tag == "-spotlight") {
+      throw std::runtime_error(tag + ": light type outside the MI355X device's scope (SURVEY.md §2 row 13)");
+    } else if (tag == "-trianglelight") {
+      const yrt_v3 P = cin.getV3(), U = cin.getV3(), V = cin.getV3(), L = cin.getV3();
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "trianglelight"), "rtNewLight");
+      check(dev, yrtSetFloat3(dev, l, "v0", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "v1", P.x + U.x, P.y + U.y, P.z + U.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "v2", P.x + V.x, P.y + V.y, P.z + V.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "L", L.x, L.y, L.z), "rtSetFloat3");
+      addLight(l);
+    } else if (tag == "-quadlight") {
+      // renderer.cpp:1118-1140
+      const yrt_v3 P = cin.getV3(), U = cin.getV3(), V = cin.getV3(), L = cin.getV3();
+      YRTHandle l0 = checkH(dev, yrtNewLight(dev, "trianglelight"), "rtNewLight");
+      check(dev, yrtSetFloat3(dev, l0, "v0", P.x + U.x + V.x, P.y + U.y + V.y, P.z + U.z + V.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l0, "v1", P.x + U.x, P.y + U.y, P.z + U.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l0, "v2", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l0, "L", L.x, L.y, L.z), "rtSetFloat3");
+      addLight(l0);
+      YRTHandle l1 = checkH(dev, yrtNewLight(dev, "trianglelight"), "rtNewLight");
+      check(dev, yrtSetFloat3(dev, l1, "v0", P.x + U.x + V.x, P.y + U.y + V.y, P.z + U.z + V.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l1, "v1", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l1, "v2", P.x + V.x, P.y + V.y, P.z + V.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l1, "L", L.x, L.y, L.z), "rtSetFloat3");
+      addLight(l1);
+    } else if (tag == "-hdrilight") {
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "hdrilight"), "rtNewLight");
+      const yrt_v3 L = cin.getV3();
+      check(dev, yrtSetFloat3(dev, l, "L", L.x, L.y, L.z), "rtSetFloat3");
+      check(dev, yrtSetImage(dev, l, "image", loader->image(path + cin.get())), "rtSetImage");
+      addLight(l);
+    } else if (tag == "-vp") camPos = cin.getV3();
+    else if (tag == "-vi") camLookAt = cin.getV3();
+    else if (tag == "-vd") { yrt_v3 d = cin.getV3(); camLookAt = {camPos.x + d.x, camPos.y + d.y, camPos.z + d.z}; }
+    else if (tag == "-vu") camUp = cin.getV3();
+    else if (tag == "-angle" || tag == "-fov") camFieldOfView = cin.getFloat();
+    else if (tag == "-radius") {
+      camRadius = cin.getFloat();
+      if (camRadius != 0.0f) throw std::runtime_error("-radius (depth-of-field camera) is outside the MI355X device's scope");
+    } else if (tag == "-stereo") stereo = true;
+    else if (tag == "-toeIn") toeIn = true;
+    else if (tag == "-waterMark") waterMark = true;
+    else if (tag == "-eyeSeparation") eyeSeparation = cin.getFloat();
+    else if (tag == "-zeroParallax") zeroParallaxDistance = cin.getFloat();
+    else if (tag == "-size") {
+      width = cin.getInt();
+      height = cin.getInt();
+      frameBuffer = checkH(dev, yrtNewFrameBuffer(dev, format.c_str(), width, height, numBuffers, nullptr), "rtNewFrameBuffer");
+    } else if (tag == "-jpegQuality") {
+      jpegQuality = std::max(1, std::min(100, cin.getInt()));
+    } else if (tag == "-framebuffer" || tag == "-fb") {
+      format = cin.get();
+      frameBuffer = checkH(dev, yrtNewFrameBuffer(dev, format.c_str(), width, height, numBuffers, nullptr), "rtNewFrameBuffer");
+    } else if (tag == "-fullscreen" || tag == "-display") {
+      if (tag == "-display") outFileName = "";
+    } else if (tag == "-refine") cin.getInt();
+    else if (tag == "-scene") sceneType = cin.get();
+    else if (tag == "-accel") accel = cin.get();
+    else if (tag == "-builder") builder = cin.get();
+    else if (tag == "-traverser") traverser = cin.get();
+    else if (tag == "-renderer") {
+      const std::string r = cin.get();
+      if (r == "debug") {
+        // parseDebugRenderer (renderer.cpp:393-412)
+        newRendererPathTracer("debug");
+      } else if (r == "pt" || r == "pathtracer") {
+        newRendererPathTracer("pathtracer");
+      } else {
+        throw std::runtime_error("(when parsing -renderer) : unknown renderer: " + r);
+      }
+      if (cin.peek() == "{") {
+        cin.drop();
+        while (cin.peek() != "}" && cin.peek() != "") {
+          const std::string t = cin.get();
+          cin.force("=");
+          if (t == "depth") check(dev, yrtSetInt1(dev, renderer, "maxDepth", cin.getInt()), "rtSetInt1");
+          else if (t == "tMaxShadowRay" && r != "debug")
+            check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowRay", cin.getFloat() * sceneScale), "rtSetFloat1");
+          else if (t == "spp" && r != "debug") check(dev, yrtSetInt1(dev, renderer, "sampler.spp", cin.getInt()), "rtSetInt1");
+          else if (t == "minContribution" && r != "debug")
+            check(dev, yrtSetFloat1(dev, renderer, "minContribution", cin.getFloat()), "rtSetFloat1");
+          else if (t == "backplate") throw std::runtime_error("backplate images are outside the MI355X device's scope");
+          else cin.get();  // unknown tag (reference prints a warning)
+        }
+        cin.drop();
+      }
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    } else if (tag == "-gamma") {
+      gamma = cin.getFloat();
+      check(dev, yrtSetFloat1(dev, tonemapper, "gamma", gamma), "rtSetFloat1");
+      check(dev, yrtCommit(dev, tonemapper), "rtCommit(tonemapper)");
+    } else if (tag == "-vignetting") {
+      vignetting = cin.getInt() != 0;
+      check(dev, yrtSetBool1(dev, tonemapper, "vignetting", vignetting), "rtSetBool1");
+      check(dev, yrtCommit(dev, tonemapper), "rtCommit(tonemapper)");
+    } else if (tag == "-depth") {
+      depth = cin.getInt();
+      check(dev, yrtSetInt1(dev, renderer, "maxDepth", depth), "rtSetInt1");
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    } else if (tag == "-tMaxShadowRay") {
+      tMaxShadowRay = cin.getFloat() * sceneScale;
+      check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowRay", tMaxShadowRay), "rtSetFloat1");
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    } else if (tag == "-tMaxShadowJitter") {
+      tMaxShadowJitter = cin.getFloat();
+      check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowJitter", tMaxShadowJitter), "rtSetFloat1");
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    } else if (tag == "-faceCullingMode") {
+      faceCullingMode = cin.get();
+    } else if (tag == "-spp") {
+      spp = cin.getInt();
+      check(dev, yrtSetInt1(dev, renderer, "sampler.spp", spp), "rtSetInt1");
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    } else if (tag == "-backplate") {
+      throw std::runtime_error("backplate images are outside the MI355X device's scope");
+    } else if (tag == "-frames") {
+      numFrames = cin.getInt();
+    } else if (tag == "-o") {
+      const std::string fn = cin.get();
+      outFileName = (!fn.empty() && fn[0] == '/') ? fn : path + fn;
+    } else if (tag == "-threads" || tag == "-device" || tag == "-rtcore") {
+      cin.get();
+    } else if (tag == "-regression") {
+      throw std::runtime_error("-regression (interactive GLUT mode) is out of scope");
+    } else {
+      throw std::runtime_error("unknown command line parameter: " + tag);
+    }
+  }
+}
+
+// createCamera (renderer.cpp:309-332) / stereo faces (renderer.cpp:747-757)
+YRTHandle RtState::createCamera(int face) {
+  auto it = cameras.find(face);
+  if (it != cameras.end()) return it->second;
+  const yrt_affine space = look_at(camPos, camLookAt, camUp);
+  YRTHandle c;
+  if (face < 0) {
+    c = checkH(dev, yrtNewCamera(dev, "pinhole"), "rtNewCamera");
+    check(dev, yrtSetTransform(dev, c, "local2world", space.v), "rtSetTransform");
+    check(dev, yrtSetFloat1(dev, c, "angle", camFieldOfView), "rtSetFloat1");
+    check(dev, yrtSetFloat1(dev, c, "aspectRatio", float(width) / float(height)), "rtSetFloat1");
+  } else {
+    c = checkH(dev, yrtNewCamera(dev, "stereo"), "rtNewCamera");
+    check(dev, yrtSetTransform(dev, c, "local2world", space.v), "rtSetTransform");
+    check(dev, yrtSetInt1(dev, c, "cubeFaceIndex", face), "rtSetInt1");
+    check(dev, yrtSetFloat3(dev, c, "origin", camPos.x, camPos.y, camPos.z), "rtSetFloat3");
+    check(dev, yrtSetFloat3(dev, c, "lookAt", camLookAt.x, camLookAt.y, camLookAt.z), "rtSetFloat3");
+    check(dev, yrtSetFloat3(dev, c, "up", camUp.x, camUp.y, camUp.z), "rtSetFloat3");
+    check(dev, yrtSetBool1(dev, c, "toeIn", toeIn), "rtSetBool1");
+  }
+  check(dev, yrtCommit(dev, c), "rtCommit(camera)");
+  return cameras[face] = c;
+}
+
+// createScene (renderer.cpp:335-345)
+YRTHandle RtState::createScene() {
+  if (scene) return scene;
+  scene = checkH(dev, yrtNewScene(dev, sceneType.c_str()), "rtNewScene");
+  check(dev, yrtSetString(dev, scene, "accel", accel.c_str()), "rtSetString");
+  check(dev, yrtSetString(dev, scene, "builder", builder.c_str()), "rtSetString");
+  check(dev, yrtSetString(dev, scene, "traverser", traverser.c_str()), "rtSetString");
+  for (size_t i = 0; i < prims.size(); i++) check(dev, yrtSetPrimitive(dev, scene, i, prims[i]), "rtSetPrimitive");
+  check(dev, yrtCommit(dev, scene), "rtCommit(scene)");
+  return scene;
+}
+
+static int fb_format(const std::string& f) {
+  if (f == "RGB8") return 0;
+  if (f == "RGBA8") return 1;
+  if (f == "RGB_FLOAT32") return 2;
+  return 3;
+}
+static size_t fb_stride(int fmt, int w) {
+  switch (fmt) {
+    case 0: return (3 * (size_t)w + 3) / 4 * 4;
+    case 1: return 4 * (size_t)w;
+    case 2: return 12 * (size_t)w;
+    default: return 16 * (size_t)w;
+  }
+}
+
+// ---------------------------------------------------------------- image store
+static void write_png(const std::string& file, int w, int h, const std::vector<uint8_t>& rgb) {
+  std::vector<uint8_t> raw;
+  raw.reserve((size_t)(3 * w + 1) * h);
+  for (int y = 0; y < h; ++y) {
+    raw.push_back(0);
+    raw.insert(raw.end(), rgb.begin() + (size_t)y * w * 3, rgb.begin() + (size_t)(y + 1) * w * 3);
+  }
+  uLongf zl = compressBound(raw.size());
+  std::vector<uint8_t> z(zl);
+  compress2(z.data(), &zl, raw.data(), raw.size(), 6);
+  z.resize(zl);
+  FILE* f = fopen(file.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot write " + file);
+  auto be = [](uint32_t v, uint8_t* o) { o[0] = v >> 24; o[1] = v >> 16; o[2] = v >> 8; o[3] = v; };
+  auto chunk = [&](const char* t, const std::vector<uint8_t>& d) {
+    uint8_t b[4];
+    be((uint32_t)d.size(), b);
+    fwrite(b, 1, 4, f);
+    fwrite(t, 1, 4, f);
+    if (!d.empty()) fwrite(d.data(), 1, d.size(), f);
+    uLong c = crc32(0, (const Bytef*)t, 4);
+    if (!d.empty()) c = crc32(c, d.data(), d.size());
+    be((uint32_t)c, b);
+    fwrite(b, 1, 4, f);
+  };
+  static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+  fwrite(sig, 1, 8, f);
+  std::vector<uint8_t> ihdr(13, 0);
+  be(w, &ihdr[0]);
+  be(h, &ihdr[4]);
+  ihdr[8] = 8;
+  ihdr[9] = 2;
+  chunk("IHDR", ihdr);
+  chunk("IDAT", z);
+  chunk("IEND", {});
+  fclose(f);
+}
+
+void store_image(const std::string& file, int w, int h, int fmt, const void* px, size_t stride) {
+  const std::string ext = ext_of(file);
+  if (ext == "pfm") {
+    FILE* f = fopen(file.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + file);
+    fprintf(f, "PF\n%d %d\n-1\n", w, h);
+    for (int y = h - 1; y >= 0; --y)
+      for (int x = 0; x < w; ++x) {
+        float c[3];
+        const uint8_t* row = (const uint8_t*)px + (size_t)y * stride;
+        if (fmt >= 2) {
+          const float* p = (const float*)row + x * (fmt == 2 ? 3 : 4);
+          c[0] = p[0]; c[1] = p[1]; c[2] = p[2];
+        } else {
+          const uint8_t* p = row + x * (fmt == 0 ? 3 : 4);
+          for (int k = 0; k < 3; ++k) c[k] = p[k] / 255.0f;
+        }
+        fwrite(c, 4, 3, f);
+      }
+    fclose(f);
+    return;
+  }
+  std::vector<uint8_t> rgb((size_t)w * h * 3);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const uint8_t* row = (const uint8_t*)px + (size_t)y * stride;
+      uint8_t* o = &rgb[((size_t)y * w + x) * 3];
+      if (fmt >= 2) {
+        const float* p = (const float*)row + x * (fmt == 2 ? 3 : 4);
+        for (int k = 0; k < 3; ++k) o[k] = (uint8_t)(std::max(0.0f, std::min(p[k], 1.0f)) * 255.0f);
+      } else {
+        const uint8_t* p = row + x * (fmt == 0 ? 3 : 4);
+        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+      }
+    }
+  if (ext == "ppm") {
+    FILE* f = fopen(file.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + file);
+    fprintf(f, "P6\n%d %d\n255\n", w, h);
+    fwrite(rgb.data(), 1, rgb.size(), f);
+    fclose(f);
+  } else if (ext == "png") {
+    write_png(file, w, h, rgb);
+  } else {
+    throw std::runtime_error("image format ." + ext + " not supported by this build (JPEG output: SURVEY §8(f) rank 2)");
+  }
+}
+
+// outputMode (renderer.cpp:508-905)
+void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outImage) {
+  if (!renderer) throw std::runtime_error("no renderer set");
+  const int fmt = fb_format(format);
+  const size_t stride = fb_stride(fmt, width);
+  YRTHandle sc = createScene();
+  if (stereo) {
+    // non-FPR stereo branch (:742-878): 12 faces, strip = right eye first, each L,R,U,D,B,F
+    std::vector<std::vector<uint8_t>> faces(12);
+    for (int i = 0; i < 12; ++i) {
+      YRTHandle cam = createCamera(i);
+      check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
+      for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
+      const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
+      faces[i].assign(p, p + stride * height);
+      check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+      if (stopFlag && stopFlag->load()) return;
+    }
+    const int bpp = fmt == 0 ? 3 : fmt == 1 ? 4 : fmt == 2 ? 12 : 16;
+    const size_t sstride = (size_t)bpp * width * 12;
+    std::vector<uint8_t> strip(sstride * height);
+    static const int seg2face[6] = {3, 1, 4, 5, 2, 0};
+    for (int y = 0; y < height; ++y)
+      for (int seg = 0; seg < 12; ++seg) {
+        const int eye = seg / 6 == 0 ? 1 : 0;
+        const int face = 6 * eye + seg2face[seg % 6];
+        memcpy(&strip[(size_t)y * sstride + (size_t)seg * width * bpp], &faces[face][(size_t)y * stride],
+               (size_t)width * bpp);
+      }
+    if (!fileName.empty()) store_image(fileName, width * 12, height, fmt, strip.data(), sstride);
+    if (outImage) *outImage = strip;
+  } else {
+    YRTHandle cam = createCamera(-1);
+    check(dev, yrtSetInt1(dev, renderer, "showprogress", 1), "rtSetInt1");
+    check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
+    for (int i = 0; i < numFrames; i++)
+      check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
+    for (int i = 0; i < numBuffers; i++) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
+    const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
+    if (!fileName.empty()) store_image(fileName, width, height, fmt, p, stride);
+    if (outImage) outImage->assign(p, p + stride * height);
+    check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+  }
+}
+
+}  // namespace yrtfe

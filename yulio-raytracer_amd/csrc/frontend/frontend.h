@@ -1,0 +1,123 @@
+// frontend.h — internals of the front-end library (loaders, command line, outputs).
+#pragma once
+
+#include <math.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../../include/yrt_device.h"
+
+namespace yrtfe {
+
+struct yrt_v3 {
+  float x, y, z;
+};
+
+// AffineSpace3f in the rtSetTransform 12-float layout (vx, vy, vz, p); products follow
+// common/math/affinespace.h / linearspace3.h operation order.
+struct yrt_affine {
+  float v[12];
+  static yrt_affine identity() {
+    yrt_affine a = {{1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0}};
+    return a;
+  }
+  static yrt_affine translate(float x, float y, float z) {
+    yrt_affine a = identity();
+    a.v[9] = x; a.v[10] = y; a.v[11] = z;
+    return a;
+  }
+  static yrt_affine scale(float x, float y, float z) {
+    yrt_affine a = {{x, 0, 0, 0, y, 0, 0, 0, z, 0, 0, 0}};
+    return a;
+  }
+  static yrt_affine rotate(float ux, float uy, float uz, float r) {
+    const float l = 1.0f / sqrtf(ux * ux + uy * uy + uz * uz);
+    ux *= l; uy *= l; uz *= l;
+    const float s = sinf(r), c = cosf(r);
+    // rows of LinearSpace3::rotate (linearspace3.h:95-101) stored as columns
+    const float m00 = ux * ux + (1 - ux * ux) * c, m01 = ux * uy * (1 - c) - uz * s, m02 = ux * uz * (1 - c) + uy * s;
+    const float m10 = ux * uy * (1 - c) + uz * s, m11 = uy * uy + (1 - uy * uy) * c, m12 = uy * uz * (1 - c) - ux * s;
+    const float m20 = ux * uz * (1 - c) - uy * s, m21 = uy * uz * (1 - c) + ux * s, m22 = uz * uz + (1 - uz * uz) * c;
+    yrt_affine a = {{m00, m10, m20, m01, m11, m21, m02, m12, m22, 0, 0, 0}};
+    return a;
+  }
+  yrt_v3 lin(float x, float y, float z) const {
+    return {x * v[0] + y * v[3] + z * v[6], x * v[1] + y * v[4] + z * v[7], x * v[2] + y * v[5] + z * v[8]};
+  }
+  yrt_v3 point(float x, float y, float z) const {
+    yrt_v3 l = lin(x, y, z);
+    return {l.x + v[9], l.y + v[10], l.z + v[11]};
+  }
+  yrt_affine operator*(const yrt_affine& b) const {
+    yrt_affine r;
+    for (int c = 0; c < 3; ++c) {
+      yrt_v3 col = lin(b.v[3 * c], b.v[3 * c + 1], b.v[3 * c + 2]);
+      r.v[3 * c] = col.x; r.v[3 * c + 1] = col.y; r.v[3 * c + 2] = col.z;
+    }
+    yrt_v3 p = point(b.v[9], b.v[10], b.v[11]);
+    r.v[9] = p.x; r.v[10] = p.y; r.v[11] = p.z;
+    return r;
+  }
+};
+
+// lookAtPoint (common/math/affinespace.h:72-77)
+yrt_affine look_at(yrt_v3 eye, yrt_v3 point, yrt_v3 up);
+
+std::string path_of(const std::string& f);
+std::string ext_of(const std::string& f);
+std::string join_path(const std::string& dir, const std::string& f);
+void check(YRTDevice dev, int rc, const char* what);
+YRTHandle checkH(YRTDevice dev, YRTHandle h, const char* what);
+
+struct Loader {
+  YRTDevice dev;
+  std::map<std::string, YRTHandle> images, textures;
+  explicit Loader(YRTDevice d) : dev(d) {}
+  YRTHandle image(const std::string& file);
+  YRTHandle texture(const std::string& file, const std::string& filtering = "bilinear", bool invert = false);
+  std::vector<YRTHandle> loadScene(const std::string& file);
+};
+
+// Global render state of devices/renderer/renderer.cpp:240-300, one per session.
+struct RtState {
+  YRTDevice dev = nullptr;
+  bool ownsDevice = false;
+  yrt_v3 camPos{0, 0, 0}, camLookAt{1, 0, 0}, camUp{0, 1, 0};
+  float camFieldOfView = 64.0f, camRadius = 0.0f;
+  bool stereo = false, toeIn = false, waterMark = false, debugging = false;
+  float eyeSeparation = 6.35f * 0.393701f;
+  float zeroParallaxDistance = 6.35f * 0.393701f * 30.f;
+  float tMaxShadowRay = INFINITY, tMaxShadowJitter = .2f, sceneScale = 1.f;
+  std::string faceCullingMode = "default";
+  YRTHandle renderer = nullptr, tonemapper = nullptr, frameBuffer = nullptr, scene = nullptr;
+  std::vector<YRTHandle> prims;
+  std::map<int, YRTHandle> cameras;
+  std::string sceneType = "default", accel = "default", builder = "default", traverser = "default";
+  int depth = -1, spp = 1, numBuffers = 1;
+  float gamma = 1.0f;
+  bool vignetting = false;
+  int width = 512, height = 512;
+  std::string format = "RGB8";
+  std::string outFileName;
+  int numFrames = 1, jpegQuality = 90;
+  std::atomic<bool>* stopFlag = nullptr;
+  void* statusCallback = nullptr;
+  void* statusUser = nullptr;
+  std::unique_ptr<Loader> loader;
+
+  void createGlobalObjects();
+  void parseCommandLine(const std::vector<std::string>& tokens, const std::string& path);
+  YRTHandle createCamera(int face);
+  YRTHandle createScene();
+  void outputMode(const std::string& file, std::vector<uint8_t>* outImage = nullptr);
+};
+
+std::vector<std::string> tokenize_args(int argc, const char** argv);
+void store_image(const std::string& file, int w, int h, int format, const void* pixels, size_t stride);
+
+}  // namespace yrtfe

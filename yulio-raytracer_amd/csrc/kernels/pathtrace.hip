@@ -1,0 +1,847 @@
+// pathtrace.hip — wavefront path tracer for gfx950 (MI355X).
+//
+// The reference's per-pixel integrator (integrators/pathtraceintegrator.cpp:50-217 called
+// from renderers/integratorrenderer.cpp:118-185) becomes, per batch of pixels x spp paths:
+//
+//   k_raygen -> for depth d: k_trace_closest -> k_shade -> k_trace_any -> k_shadow_resolve
+//            -> k_resolve_pixels
+//
+// Queues are compacted with one wave-wide ballot/prefix + one atomic per wave.  Per-path
+// radiance is accumulated in the same order as the reference's sequential loop (env or
+// emission first, then the direct-light terms in light order), and the pixel sum over
+// samples runs s = 0..spp-1, so results do not depend on queue order.
+//
+// Wave64: every cross-lane primitive below is written for 64 lanes (ballot is 64-bit).
+
+#include <hip/hip_runtime.h>
+
+#include "yrt_kernels.h"
+#include "yrt_shade.h"
+#include "yrt_traverse.h"
+
+namespace yrt {
+
+#define YRT_BLOCK 256
+
+// ---------------------------------------------------------------- wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Reserve k slots (k >= 0 per lane) in *counter; returns this lane's first slot.
+// Every lane of the wave must call it (no divergent callers).
+__device__ __forceinline__ unsigned wave_reserve(unsigned* counter, unsigned k) {
+  const int lane = lane_id();
+  unsigned incl = k;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    unsigned y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const unsigned total = __shfl(incl, 63, 64);
+  unsigned base = 0;
+  if (lane == 0 && total) base = atomicAdd(counter, total);
+  base = __shfl(base, 0, 64);
+  return base + incl - k;
+}
+
+__device__ __forceinline__ unsigned wave_append(unsigned* counter, bool pred, bool& got) {
+  const unsigned long long mask = __ballot(pred);
+  got = pred;
+  if (mask == 0) return 0;
+  const int lane = lane_id();
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(mask));
+  base = __shfl(base, leader, 64);
+  return base + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
+// ---------------------------------------------------------------- reference RNG
+// Park-Miller minimal standard + Bays-Durham shuffle (common/math/random.h:24-78).
+struct DevRandom {
+  int seed, state;
+  int table[32];
+  __device__ void setSeed(int s) {
+    const int a = 16807, m = 2147483647, q = 127773, r = 2836;
+    if (s == 0) seed = 1;
+    else if (s < 0) seed = -s;
+    else seed = s;
+    for (int j = 32 + 7; j >= 0; j--) {
+      int k = seed / q;
+      seed = a * (seed - k * q) - r * k;
+      if (seed < 0) seed += m;
+      if (j < 32) table[j] = seed;
+    }
+    state = table[0];
+  }
+  __device__ int getInt() {
+    const int a = 16807, m = 2147483647, q = 127773, r = 2836;
+    int k = seed / q;
+    seed = a * (seed - k * q) - r * k;
+    if (seed < 0) seed += m;
+    int j = state / (1 + (2147483647 - 1) / 32);
+    state = table[j];
+    table[j] = seed;
+    return state;
+  }
+  __device__ int getInt(int limit) { return getInt() % limit; }
+  __device__ float getFloat() { return fminf(getInt() / 2147483647.0f, 1.0f - kUlp); }
+};
+
+// Counter-based replacement for C rand() in the shadow-ray jitter
+// (pathtraceintegrator.cpp:151; the reference calls rand() from worker threads, so it
+// is not reproducible). Same function in oracle/yrt_oracle.c: hash_u01.
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x7feb352dU; h ^= h >> 15; h *= 0x846ca68bU; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ float hash_u01(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t depthLight) {
+  uint32_t h = mix32(seed ^ 0x9e3779b9U);
+  h = mix32(h ^ pixel);
+  h = mix32(h ^ (sample * 0x85ebca6bU));
+  h = mix32(h ^ (depthLight * 0xc2b2ae35U));
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ V3 ld3(const float4& p) { return v3(p.x, p.y, p.z); }
+__device__ __forceinline__ A3 ldA3(const float* m) {
+  return a3(l3(v3(m[0], m[1], m[2]), v3(m[3], m[4], m[5]), v3(m[6], m[7], m[8])), v3(m[9], m[10], m[11]));
+}
+
+// ---------------------------------------------------------------- cameras
+// PinHoleCamera::ray (cameras/pinholecamera.h:23-25)
+// StereoCubeCamera::ray (cameras/StereoCubeCamera.h:68-161)
+__device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3& dir) {
+  if (cam.type == CAM_PINHOLE) {
+    A3 p2w = ldA3(cam.p2w[0]);
+    org = p2w.p;
+    dir = normalize(fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
+    return;
+  }
+  const A3 pixel2world = ldA3(cam.p2w[0]);
+  const int eyeCubeFaceIndex = cam.cubeFaceIndex % 6;
+  const float yPixel = 1.0f - fy;
+  A3 p2w = ldA3(cam.p2w[eyeCubeFaceIndex]);
+  const V3 xyzStraight = ld3(cam.xyzStraight);
+  float theta = 0.f;
+  float absoluteVerticalAngle = 0.f;
+  if (eyeCubeFaceIndex <= 3) {
+    const V3 xDir = normalize(fx * pixel2world.l.vx + .5f * pixel2world.l.vy + pixel2world.l.vz);
+    theta = acosf(clampf(dot(xDir, xyzStraight), -1.f, 1.f)) * signf_(fx - .5f);
+    const V3 yDir = normalize(.5f * pixel2world.l.vx + yPixel * pixel2world.l.vy + pixel2world.l.vz);
+    const float yAngle = rad2deg(acosf(clampf(dot(yDir, xyzStraight), -1.f, 1.f))) * signf_(yPixel - .5f);
+    absoluteVerticalAngle = fabsf(yAngle);
+  } else {
+    const V3 xyDir = v3(fx - .5f, yPixel - .5f, 0.f);
+    const V3 xyDirNorm = normalize(xyDir);
+    const V3 xyUp = v3(0.f, eyeCubeFaceIndex == 4 ? -1.f : 1.f, 0.f);
+    theta = acosf(clampf(dot(xyDirNorm, xyUp), -1.f, 1.f)) * signf_(fx - .5f);
+    const V3 xyzDir = normalize(fx * pixel2world.l.vx + yPixel * pixel2world.l.vy + pixel2world.l.vz);
+    const float xyzAngle = rad2deg(acosf(clampf(dot(xyzDir, xyzStraight), -1.f, 1.f)));
+    absoluteVerticalAngle = 90.f - fabsf(xyzAngle);
+  }
+  float eyeOffset = cam.eyeSeparation * (cam.cubeFaceIndex < 6 ? -.5f : .5f);
+  if (absoluteVerticalAngle > cam.falloffAngle) {
+    const float coef = 1.f - smoothstepf(0.f, 1.f, smoothstepf(cam.falloffAngle, 90.f, absoluteVerticalAngle));
+    eyeOffset *= coef;
+  }
+  p2w = mul(p2w, a3_translate(v3(eyeOffset, 0.f, 0.f)));
+  const V3 origin = ld3(cam.origin), up = ld3(cam.up);
+  const A3 rayRotationSpace = a3_rotate_about(origin, up, theta);
+  const V3 rayOrigin = mul(rayRotationSpace, p2w).p;
+  if (cam.toeIn) {
+    const float toeInCorrection = -atanf(eyeOffset * cam.rcpZeroParallaxDistance);
+    p2w = mul(a3_rotate_about(rayOrigin, up, toeInCorrection), p2w);
+  }
+  org = rayOrigin;
+  dir = normalize(fx * p2w.l.vx + yPixel * p2w.l.vy + p2w.l.vz);
+}
+
+// ---------------------------------------------------------------- batch pixel mapping
+__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y) {
+  const int tile = bi.tileOffset + (bi.firstTile + (i >> 8)) * bi.tileStride;
+  const int within = i & 255;
+  if (tile >= rp.numTilesX * rp.numTilesY) return false;
+  x = (tile % rp.numTilesX) * 16 + (within & 15);
+  y = (tile / rp.numTilesX) * 16 + (within >> 4);
+  return x < rp.width && y < rp.height;
+}
+
+__device__ __forceinline__ float samp(const FrameView& fv, int dim, int rec) {
+  return fv.samples[(size_t)dim * fv.numRecords + rec];
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void k_pixel_sets(const GpuRenderParams* __restrict__ rpp, uint8_t* __restrict__ sets) {
+  const GpuRenderParams rp = *rpp;
+  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= rp.numTilesX * rp.numTilesY) return;
+  const int tile_x = (tile % rp.numTilesX) * 16;
+  const int tile_y = (tile / rp.numTilesX) * 16;
+  DevRandom rng;
+  rng.setSeed(tile_x * 91711 + tile_y * 81551 + 3433 * 0);
+  for (int dy = 0; dy < 16; dy++) {
+    const int y = tile_y + dy;
+    if (y >= rp.height) continue;
+    for (int dx = 0; dx < 16; dx++) {
+      const int x = tile_x + dx;
+      if (x >= rp.width) continue;
+      sets[(size_t)y * rp.width + x] = (uint8_t)rng.getInt(rp.sets);
+    }
+  }
+}
+
+__global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers pb, BatchInfo bi) {
+  const GpuRenderParams& rp = *fv.rp;
+  const GpuCamera& cam = *fv.cam;
+  const int P = bi.numPixels * rp.spp;
+  for (int base = blockIdx.x * blockDim.x; base < P; base += gridDim.x * blockDim.x) {
+    const int p = base + threadIdx.x;
+    bool valid = false;
+    V3 org = v3s(0.f), dir = v3s(0.f);
+    if (p < P) {
+      const int s = p / bi.numPixels, i = p - s * bi.numPixels;
+      int x, y;
+      valid = batch_pixel(rp, bi, i, x, y);
+      pb.L[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (valid) {
+        const int set = fv.pixelSets[(size_t)y * rp.width + x];
+        const int rec = set * rp.spp + s;
+        const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
+        const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
+        camera_ray(cam, fx, fy, org, dir);
+        pb.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);
+        pb.meta[p] = (0) | (0 << 8) | (1 << 9);
+      }
+      // loop head of Li: depth < maxDepth and max(throughput)=1 >= minContribution
+      valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
+    }
+    bool got;
+    const unsigned q = wave_append(&pb.counters[0], valid, got);
+    if (got) {
+      pb.qPath[0][q] = p;
+      pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
+      pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
+    }
+  }
+}
+
+template <bool ANY>
+__global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const float4* __restrict__ org,
+                                                         const float4* __restrict__ dir,
+                                                         const unsigned* __restrict__ countp,
+                                                         float4* __restrict__ hitOut, int* __restrict__ occOut) {
+  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  const int n = (int)*countp;
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    if (q >= n) break;
+    const float4 o = org[q], d = dir[q];
+    RayPre r;
+    r.org = v3(o.x, o.y, o.z);
+    r.dir = v3(d.x, d.y, d.z);
+    r.inv = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+    r.tnear = o.w;
+    r.tfar = d.w;
+    const Hit h = traverse<ANY>(sv.nodes, sv.tris, r, stack + threadIdx.x);
+    if (ANY) occOut[q] = h.tri >= 0 ? 1 : 0;
+    else hitOut[q] = make_float4(h.t, h.u, h.v, __int_as_float(h.tri));
+  }
+}
+
+// ---------------------------------------------------------------- shading helpers
+// BackendSceneFlat::postIntersect -> Shape::postIntersect
+__device__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
+                               bool wantTangents) {
+  const int g = sv.triGeom[gid];
+  const GpuGeom geom = sv.geoms[g];
+  dg.material = geom.material;
+  dg.light = geom.light;
+  dg.illumMask = geom.illumMask;
+  dg.shadowMask = geom.shadowMask;
+  dg.P = org + t * dir;
+  if (geom.kind == GEOM_TRIANGLE) {
+    // shapes/triangle.h:69-78
+    dg.Ng = v3(geom.Ng[0], geom.Ng[1], geom.Ng[2]);
+    dg.Ns = dg.Ng;
+    dg.s = u;
+    dg.t = v;
+    dg.Tx = dg.Ty = v3s(0.f);
+  } else {
+    const int4 idx = sv.indices[gid];
+    const V3 p0 = ld3(sv.positions[idx.x]), p1 = ld3(sv.positions[idx.y]), p2 = ld3(sv.positions[idx.z]);
+    const float w = 1.0f - u - v;
+    const V3 dPdu = p1 - p0, dPdv = p2 - p0;
+    dg.Ng = normalize(cross(p0 - p1, p2 - p0));  // ray.Ng (unnormalized Embree Ng)
+    if (geom.kind == GEOM_MESH_NORMALS) {
+      // shapes/trianglemesh_normals.cpp:125-147
+      dg.s = u;
+      dg.t = v;
+      const V3 n0 = ld3(sv.normals[idx.x]), n1 = ld3(sv.normals[idx.y]), n2 = ld3(sv.normals[idx.z]);
+      V3 Ns = w * n0 + u * n1 + v * n2;
+      const float len2 = dot(Ns, Ns);
+      Ns = len2 > 0 ? Ns * rsqrtf_(len2) : dg.Ng;
+      if (dot(Ns, dg.Ng) < 0) Ns = -Ns;
+      dg.Ns = Ns;
+      dg.Tx = dPdu;
+      dg.Ty = dPdv;
+    } else {
+      // shapes/trianglemesh_full.cpp:192-260
+      float dsdu, dtdu, dsdv, dtdv;
+      if (geom.flags & GF_TEXCOORDS) {
+        const float2 st0 = sv.texcoords[idx.x], st1 = sv.texcoords[idx.y], st2 = sv.texcoords[idx.z];
+        dg.s = st0.x * w + st1.x * u + st2.x * v;
+        dg.t = st0.y * w + st1.y * u + st2.y * v;
+        dsdu = st1.x - st0.x; dtdu = st1.y - st0.y;
+        dsdv = st2.x - st0.x; dtdv = st2.y - st0.y;
+      } else {
+        dg.s = u;
+        dg.t = v;
+        dsdu = 1; dtdu = 0;
+        dsdv = 0; dtdv = 1;
+      }
+      if (geom.flags & GF_NORMALS) {
+        const V3 n0 = ld3(sv.normals[idx.x]), n1 = ld3(sv.normals[idx.y]), n2 = ld3(sv.normals[idx.z]);
+        V3 Ns = w * n0 + u * n1 + v * n2;
+        const float len2 = dot(Ns, Ns);
+        Ns = len2 > 0 ? Ns * rsqrtf_(len2) : dg.Ng;
+        if (dot(Ns, dg.Ng) < 0) Ns = -Ns;
+        dg.Ns = Ns;
+      } else {
+        dg.Ns = dg.Ng;
+      }
+      if (wantTangents) {
+        const V3 dPds = normalize(dPdu * dtdv - dPdv * dtdu);
+        dg.Tx = normalize(dPds - dot(dPds, dg.Ns) * dg.Ns);
+        const V3 dPdt = normalize(dPdv * dsdu - dPdu * dsdv);
+        dg.Ty = normalize(dPdt - dot(dPdt, dg.Ns) * dg.Ns);
+      } else {
+        dg.Tx = dg.Ty = v3s(0.f);
+      }
+    }
+  }
+  dg.error = fmaxf(fabsf(t), reduce_max(absv(dg.P)));
+}
+
+__device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V3 R, float a = 0.f, float b = 0.f,
+                                         float c = 0.f) {
+  if (bs.n < YRT_MAX_COMPS) {
+    Comp& k = bs.c[bs.n++];
+    k.kind = kind;
+    k.type = type;
+    k.R = R;
+    k.a = a;
+    k.b = b;
+    k.c = c;
+  }
+}
+
+// Material::shade for the in-scope materials (materials/*.h). May modify dg.Ns (Obj bump).
+__device__ void shade_material(const SceneView& sv, const GpuMaterial& m, DG& dg, BRDFSet& bs) {
+  bs.n = 0;
+  switch (m.type) {
+    case MAT_MATTE:
+      add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
+      break;
+    case MAT_MATTE_TEXTURED:
+      if (m.tex[0] >= 0) {
+        float c[4];
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
+        add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(c[0], c[1], c[2]));
+      }
+      break;
+    case MAT_METALLIC_PAINT:
+      // p: shadeColor[0..2], eta[3], reflection eta_ [4], layer etait [5], etati [6]
+      add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[4], 1.0f);
+      add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[5], m.p[6]);
+      break;
+    case MAT_OBJ: {
+      // p: d[0], Kd[1..3], Ks[4..6], Ns[7]; tex: map_d, map_Kd, map_Ks, map_Ns, map_Bump
+      float c[4];
+      if (m.tex[4] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[4], dg.s, dg.t, c);
+        const V3 b = v3(2.0f * c[0] - 1.0f, 2.0f * c[1] - 1.0f, 2.0f * c[2] - 1.0f);
+        dg.Ns = normalize(b.x * dg.Tx + b.y * dg.Ty + b.z * dg.Ns);
+      }
+      float d = m.p[0];
+      if (m.tex[0] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], dg.s, dg.t, c);
+        d *= c[0];
+      }
+      if (d < 1.0f) add_comp(bs, C_TRANSMISSION, BT_SPECULAR_TRANSMISSION, v3s(1.0f - d));
+      V3 Kd = d * v3(m.p[1], m.p[2], m.p[3]);
+      if (m.tex[1] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[1], dg.s, dg.t, c);
+        Kd = Kd * v3(c[0], c[1], c[2]);
+      }
+      if (Kd != v3s(0.f)) add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, Kd);
+      float Ns = m.p[7];
+      if (m.tex[3] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[3], dg.s, dg.t, c);
+        Ns *= c[0];
+      }
+      V3 Ks = d * v3(m.p[4], m.p[5], m.p[6]);
+      if (m.tex[2] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[2], dg.s, dg.t, c);
+        Ks = Ks * v3(c[0], c[1], c[2]);
+      }
+      if (Ks != v3s(0.f)) add_comp(bs, C_SPECULAR, BT_GLOSSY_REFLECTION, Ks, Ns);
+      break;
+    }
+    case MAT_UBER: {
+      // p: diffuse[0..2], s0[3..4], ds[5..6], eta[7], roughness[8], reflectivity[9],
+      //    rcpRoughness[10], eta_ = 1*rcp(eta) [11]
+      float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
+      float alpha = 1.f, opacity = 0.f;
+      if (m.tex[0] >= 0) {
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+        alpha = dc[3];
+        opacity = 1.f - alpha;
+      }
+      add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(dc[0] * alpha, dc[1] * alpha, dc[2] * alpha));
+      if (alpha < 1.f) add_comp(bs, C_CONST_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3s(opacity));
+      if (m.p[9] > 0.f) add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[11], alpha * m.p[9]);
+      else if (m.p[8] == 0.f) add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[11], alpha);
+      else add_comp(bs, C_MICROFACET, BT_GLOSSY_REFLECTION, v3s(alpha), 1.f, m.p[7], m.p[10]);
+      break;
+    }
+    case MAT_THIN_DIELECTRIC: {
+      // p: transmission[0..2], s0[3..4], ds[5..6], eta[7], thickness[8], transparency[9], eta_[10]
+      add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[10], 1.0f);
+      float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
+      if (m.tex[0] >= 0)
+        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+      const float tr = m.p[9];
+      const V3 T = v3(dc[0] * tr, dc[1] * tr, dc[2] * tr);
+      add_comp(bs, C_THIN_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3(logf(T.x), logf(T.y), logf(T.z)), m.p[10],
+               m.p[8]);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+__device__ __forceinline__ void img_get(const SceneView& sv, int image, int x, int y, float c[4]) {
+  texel(sv.images[image], sv.texels, x, y, c);
+}
+
+// HDRILight::Le (lights/hdrilight.cpp:43-71)
+__device__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
+  const A3 w2l = ldA3(lt.w2l);
+  const V3 wi = xfmVector(w2l, -wo);
+  const float theta = acosf(clampf(wi.y, -1.0f, 1.0f));
+  float phi = atan2f(-wi.z, -wi.x);
+  if (phi < 0) phi += 2.0f * kPi;
+  const float u = 1.0f - (phi * kOneOverTwoPi);
+  const float v = theta * kOneOverPi;
+  const int width = lt.hdriW, height = lt.hdriH;
+  int x = max(0, min((int)(u * width), width - 1));
+  int xNext = x + 1;
+  if (xNext == width) xNext = 0;
+  const float alpha = u * width - x;
+  int y = max(0, min((int)(v * height), height - 1));
+  int yNext = y + 1;
+  if (yNext == height) yNext = height - 1;
+  const float beta = v * height - y;
+  float c0[4], c1[4], c2[4], c3[4];
+  img_get(sv, lt.image, x, y, c0);
+  img_get(sv, lt.image, xNext, y, c1);
+  img_get(sv, lt.image, xNext, yNext, c2);
+  img_get(sv, lt.image, x, yNext, c3);
+  V3 r;
+  float* rr = &r.x;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float temp0 = beta * c3[k] + (1 - beta) * c0[k];
+    const float temp1 = beta * c2[k] + (1 - beta) * c1[k];
+    rr[k] = lt.L[k] * (alpha * temp1 + (1 - alpha) * temp0);
+  }
+  return r;
+}
+
+__device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
+  if (lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
+  return hdri_Le(sv, lt, wo);
+}
+
+// Light::sample for a non-precomputed light; returns L, sets wi/pdf.
+__device__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
+  if (lt.type == LIGHT_AMBIENT) {
+    // lights/ambientlight.h:52-65 (the bsphere tMax is overwritten by the integrator)
+    wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+    return v3(lt.L[0], lt.L[1], lt.L[2]);
+  }
+  if (lt.type == LIGHT_TRIANGLE) {
+    // lights/trianglelight.h:77-85
+    const V3 A = ld3(lt.v0), B = ld3(lt.v1), C = ld3(lt.v2);
+    const float su = sqrtf(sx);
+    const V3 d = (C + (1.0f - su) * (A - C) + (sy * su) * (B - C)) - dg.P;
+    const float tMax = length(d);
+    const float dDotNg = dot(d, ld3(lt.Ng));
+    if (dDotNg >= 0) {
+      pdf = 0.f;
+      wi = v3s(0.f);
+      return v3s(0.f);
+    }
+    wi = d * rcpf_(tMax);
+    pdf = 2.0f * tMax * tMax * tMax * rcpf_(fabsf(dDotNg));
+    return v3(lt.L[0], lt.L[1], lt.L[2]);
+  }
+  pdf = 0.f;
+  wi = v3s(0.f);
+  return v3s(0.f);
+}
+
+__global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
+                                                   int depthLevel) {
+  const GpuRenderParams& rp = *fv.rp;
+  const int n = (int)pb.counters[depthLevel * 4 + 0];
+  const int cur = depthLevel & 1;
+  const int numLights = sv.numLights;
+  unsigned* nextCount = &pb.counters[(depthLevel + 1) * 4 + 0];
+  unsigned* shadowCount = &pb.counters[depthLevel * 4 + 1];
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    const bool active = q < n;
+    int path = 0;
+    V3 org = v3s(0.f), dir = v3s(0.f), thr = v3s(0.f), L = v3s(0.f);
+    int meta = 0, depth = 0, rec = 0, pixelId = 0, s = 0;
+    bool ignoreVL = false, unbent = false, isHit = false, useDirect = false;
+    float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+    DG dg;
+    BRDFSet bs;
+    bs.n = 0;
+    V3 wo = v3s(0.f);
+    if (active) {
+      path = pb.qPath[cur][q];
+      const float4 o = pb.qOrg[cur][q], d = pb.qDir[cur][q];
+      org = v3(o.x, o.y, o.z);
+      dir = v3(d.x, d.y, d.z);
+      h = pb.hit[q];
+      const float4 t4 = pb.thr[path], l4 = pb.L[path];
+      thr = v3(t4.x, t4.y, t4.z);
+      L = v3(l4.x, l4.y, l4.z);
+      meta = pb.meta[path];
+      depth = meta & 255;
+      ignoreVL = (meta >> 8) & 1;
+      unbent = (meta >> 9) & 1;
+      s = path / bi.numPixels;
+      const int i = path - s * bi.numPixels;
+      int x = 0, y = 0;
+      batch_pixel(rp, bi, i, x, y);
+      pixelId = y * rp.width + x;
+      rec = fv.pixelSets[pixelId] * rp.spp + s;
+      wo = -dir;
+      const int gid = __float_as_int(h.w);
+      isHit = gid >= 0;
+      if (!isHit) {
+        // environment shading (pathtraceintegrator.cpp:79-92); backplate not supported
+        if (!ignoreVL)
+          for (int j = 0; j < sv.numEnvLights; ++j) L = L + thr * env_Le(sv, sv.lights[sv.envLights[j]], wo);
+      } else {
+        const int g = sv.triGeom[gid];
+        const int mat = sv.geoms[g].material;
+        const bool wantT = mat >= 0 && sv.materials[mat].type == MAT_OBJ && sv.materials[mat].tex[4] >= 0;
+        post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
+        bool backfacing = false;
+        if (dot(dg.Ng, dir) > 0.f) {
+          backfacing = true;
+          dg.Ng = -dg.Ng;
+          dg.Ns = -dg.Ns;
+        }
+        if (dg.material >= 0) shade_material(sv, sv.materials[dg.material], dg, bs);
+        if (!ignoreVL && dg.light >= 0 && !backfacing) {
+          const GpuLight& al = sv.lights[dg.light];
+          L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
+        }
+        for (int k = 0; k < YRT_MAX_COMPS; ++k)
+          if (k < bs.n) useDirect |= (bs.c[k].type & BT_DIFFUSE) != 0;
+      }
+      pb.L[path] = make_float4(L.x, L.y, L.z, 0.f);
+    }
+
+    // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167)
+    for (int li = 0; li < numLights; ++li) {
+      bool pred = false;
+      V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
+      float tnear = 0.f, tfar = 0.f;
+      if (active && isHit && useDirect) {
+        const GpuLight lt = sv.lights[li];
+        if ((lt.illumMask & dg.illumMask) != 0) {
+          V3 Ls;
+          float pdf;
+          if (lt.precomputed >= 0) {
+            const float* ls = fv.lightSamples + ((size_t)rec * fv.numLightSlots + lt.precomputed) * 8;
+            wi = v3(ls[0], ls[1], ls[2]);
+            pdf = ls[3];
+            Ls = v3(ls[4], ls[5], ls[6]);
+          } else {
+            const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
+            const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
+            Ls = light_sample(lt, dg, sx, sy, wi, pdf);
+          }
+          if (!(Ls == v3s(0.f) || pdf == 0.f)) {
+            const V3 brdf = set_eval(bs, wo, dg, wi, BT_DIFFUSE);
+            if (!(brdf == v3s(0.f))) {
+              const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
+              const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
+                                                  rp.tMaxShadowRay * rp.tMaxShadowJitter;
+              float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
+              const float dotProduct = dot(wi, ld3(rp.up));
+              if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
+              sOrg = dg.P;
+              tnear = dg.error * rp.epsilon;
+              tfar = tMax - dg.error * rp.epsilon;
+              contrib = thr * Ls * brdf * rcpf_(pdf);
+              pred = true;
+            }
+          }
+        }
+      }
+      bool got;
+      const unsigned si = wave_append(shadowCount, pred, got);
+      if (got) {
+        pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
+        pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
+        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, 0.f);
+      }
+      if (active) pb.shFirst[(size_t)q * numLights + li] = got ? (int)si : -1;
+    }
+
+    // continuation (pathtraceintegrator.cpp:169-213)
+    bool cont = false;
+    V3 nwi = v3s(0.f);
+    if (active && isHit) {
+      bool stop = depth >= rp.maxDepth - 1;
+      if (!stop && rp.rrDepth > 0 && depth >= rp.rrDepth - 1) {  // size_t compare in the reference
+        const float qrr = fminf(reduce_max(thr) * 1.f * 1.f, .95f);  // eta == 1
+        if (samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec) >= qrr) stop = true;
+      }
+      if (!stop) {
+        const int d2 = rp.firstScatterSampleID + depth;
+        const float sx = samp(fv, 5 + rp.dim1D + 2 * d2, rec);
+        const float sy = samp(fv, 5 + rp.dim1D + 2 * d2 + 1, rec);
+        const float ss = samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec);
+        float pdf;
+        uint32_t type;
+        const V3 c = set_sample(bs, wo, dg, sx, sy, ss, nwi, pdf, type);
+        if (!(c == v3s(0.f) || pdf <= 0.f)) {
+          const V3 nthr = thr * c * rcpf_(pdf);
+          const bool nIgnore = (type & BT_DIFFUSE) != 0;
+          const bool nUnbent = unbent && (nwi == dir);
+          // loop head of the next iteration: depth+1 < maxDepth holds; minContribution test
+          if (!(reduce_max(nthr) < rp.minContribution)) {
+            cont = true;
+            pb.thr[path] = make_float4(nthr.x, nthr.y, nthr.z, 0.f);
+            pb.meta[path] = (depth + 1) | ((nIgnore ? 1 : 0) << 8) | ((nUnbent ? 1 : 0) << 9);
+          }
+        }
+      }
+    }
+    bool got;
+    const unsigned nq = wave_append(nextCount, cont, got);
+    if (got) {
+      pb.qPath[cur ^ 1][nq] = path;
+      pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
+      pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
+    }
+  }
+}
+
+// Adds the unoccluded direct-light terms in light order.
+__global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, int depthLevel, int numLights) {
+  const int n = (int)pb.counters[depthLevel * 4 + 0];
+  const int cur = depthLevel & 1;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    bool any = false;
+    for (int li = 0; li < numLights; ++li) any |= pb.shFirst[(size_t)q * numLights + li] >= 0;
+    if (!any) continue;
+    const int path = pb.qPath[cur][q];
+    const float4 l4 = pb.L[path];
+    V3 L = v3(l4.x, l4.y, l4.z);
+    for (int li = 0; li < numLights; ++li) {
+      const int si = pb.shFirst[(size_t)q * numLights + li];
+      if (si < 0 || pb.sOcc[si]) continue;
+      const float4 c = pb.sContrib[si];
+      L = L + v3(c.x, c.y, c.z);
+    }
+    pb.L[path] = make_float4(L.x, L.y, L.z, 0.f);
+  }
+}
+
+// AccuBuffer::update (api/framebuffer.h:289-304) + DefaultToneMapper::eval
+// (tonemappers/defaulttonemapper.h:23-36) + FrameBufferRGB8::set (api/framebuffer.h:220-226)
+__global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, PathBuffers pb, BatchInfo bi,
+                                                            float* __restrict__ fbFloat, uint8_t* __restrict__ fbRGB8,
+                                                            int rgb8Stride, float4* __restrict__ accu, int accumulate) {
+  const GpuRenderParams& rp = *fv.rp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < bi.numPixels; i += gridDim.x * blockDim.x) {
+    int x, y;
+    if (!batch_pixel(rp, bi, i, x, y)) continue;
+    V3 L = v3s(0.f);
+    for (int s = 0; s < rp.spp; ++s) {
+      const float4 l4 = pb.L[(size_t)s * bi.numPixels + i];
+      L = L + v3(l4.x, l4.y, l4.z);
+    }
+    // AccuBuffer::update: non-accumulating frames store (L, spp), accumulating ones add
+    const size_t pix = (size_t)y * rp.width + x;
+    float4 a = make_float4(L.x, L.y, L.z, (float)rp.spp);
+    if (accumulate) {
+      const float4 c = accu[pix];
+      a = make_float4(c.x + L.x, c.y + L.y, c.z + L.z, c.w + (float)rp.spp);
+    }
+    accu[pix] = a;
+    V3 L0 = accumulate ? v3(a.x, a.y, a.z) * rcpf_(a.w) : L * rcpf_((float)rp.spp);
+    if (rp.gamma != 1.0f) L0 = v3(powf(L0.x, rp.rcpGamma), powf(L0.y, rp.rcpGamma), powf(L0.z, rp.rcpGamma));
+    if (fbFloat) {
+      float* o = fbFloat + ((size_t)y * rp.width + x) * 3;
+      o[0] = L0.x;
+      o[1] = L0.y;
+      o[2] = L0.z;
+    }
+    if (fbRGB8) {
+      uint8_t* o = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
+      o[0] = (uint8_t)clampf(L0.x * 255.0f, 0.0f, 255.0f);
+      o[1] = (uint8_t)clampf(L0.y * 255.0f, 0.0f, 255.0f);
+      o[2] = (uint8_t)clampf(L0.z * 255.0f, 0.0f, 255.0f);
+    }
+  }
+}
+
+// DebugRenderer (renderers/debugrenderer.cpp:66-140): one thread per 16x16 tile, since the
+// per-tile Random is consumed sequentially in scan order.
+__global__ __launch_bounds__(64) void k_debug(SceneView sv, FrameView fv, int maxDepth, int spp,
+                                             float* __restrict__ fbFloat, uint8_t* __restrict__ fbRGB8,
+                                             int rgb8Stride) {
+  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  const GpuRenderParams& rp = *fv.rp;
+  const GpuCamera& cam = *fv.cam;
+  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= rp.numTilesX * rp.numTilesY) return;
+  DevRandom rnd;
+  rnd.setSeed(tile * 1024);
+  const int x0 = (tile % rp.numTilesX) * 16, y0 = (tile / rp.numTilesX) * 16;
+  for (int dy = 0; dy < 16; dy++) {
+    const int iy = y0 + dy;
+    const float fy = iy * rp.rcpHeight;
+    if (iy >= rp.height) continue;
+    for (int dx = 0; dx < 16; dx++) {
+      const int ix = x0 + dx;
+      const float fx = ix * rp.rcpWidth;
+      if (ix >= rp.width) continue;
+      for (int i = 0; i < spp; i++) {
+        V3 org, dir;
+        camera_ray(cam, fx, fy, org, dir);
+        float tnear = 0.f, tfar = __int_as_float(0x7f800000);
+        Hit h;
+        h.tri = -1;
+        int id0 = -1, id1 = -1;
+        for (int depth = 0; depth < maxDepth; depth++) {
+          RayPre r;
+          r.org = org;
+          r.dir = dir;
+          r.inv = v3(safe_inv(dir.x), safe_inv(dir.y), safe_inv(dir.z));
+          r.tnear = tnear;
+          r.tfar = tfar;
+          h = traverse<false>(sv.nodes, sv.tris, r, stack + threadIdx.x);
+          if (h.tri < 0) {
+            id0 = id1 = -1;
+            break;
+          }
+          const int g = sv.triGeom[h.tri];
+          id0 = g;
+          id1 = h.tri - sv.geoms[g].triBase;
+          if (depth + 1 < maxDepth) {
+            const int4 idx = sv.indices[h.tri];
+            const V3 p0 = ld3(sv.positions[idx.x]), p1 = ld3(sv.positions[idx.y]), p2 = ld3(sv.positions[idx.z]);
+            const V3 Ng = cross(p0 - p1, p2 - p0);  // ray.Ng
+            V3 Nf = normalize(Ng);
+            if (dot(-dir, Nf) < 0) Nf = -Nf;
+            const float u1 = rnd.getFloat();
+            const float u2 = rnd.getFloat();
+            float pdf;
+            const V3 norg = org + 0.999f * h.t * dir;
+            dir = cosine_hemi(u1, u2, Nf, pdf);
+            org = norg;
+            tnear = 4.0f * kUlp;
+            tfar = __int_as_float(0x7f800000);
+          }
+        }
+        V3 c;
+        if (id0 < 0) c = v3s(1.0f);
+        else
+          c = v3(((3434553u * ((unsigned)(id0 + id1 + 3243))) % 255) / 255.0f,
+                 ((7342453u * ((unsigned)(id0 + id1 + 8237))) % 255) / 255.0f,
+                 ((9234454u * ((unsigned)(id0 + id1 + 2343))) % 255) / 255.0f);
+        if (fbFloat) {
+          float* o = fbFloat + ((size_t)iy * rp.width + ix) * 3;
+          o[0] = c.x;
+          o[1] = c.y;
+          o[2] = c.z;
+        }
+        if (fbRGB8) {
+          uint8_t* o = fbRGB8 + (size_t)iy * rgb8Stride + 3 * ix;
+          o[0] = (uint8_t)clampf(c.x * 255.0f, 0.0f, 255.0f);
+          o[1] = (uint8_t)clampf(c.y * 255.0f, 0.0f, 255.0f);
+          o[2] = (uint8_t)clampf(c.z * 255.0f, 0.0f, 255.0f);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static inline int grid_for(long long n, int block, int maxBlocks) {
+  long long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > maxBlocks) g = maxBlocks;
+  return (int)g;
+}
+
+void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int height, int sets, hipStream_t s) {
+  const int tiles = ((width + 15) / 16) * ((height + 15) / 16);
+  hipLaunchKernelGGL(k_pixel_sets, dim3((tiles + 63) / 64), dim3(64), 0, s, fv.rp, pixelSets);
+}
+
+void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s) {
+  // spp is read on device; the host passes the path count through capacity sizing.
+  hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
+}
+
+void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count,
+                          int maxCount, float4* hit, hipStream_t s) {
+  hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
+                     sv, org, dir, count, hit, (int*)nullptr);
+}
+
+void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count, int maxCount,
+                      int* occluded, hipStream_t s) {
+  hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
+                     sv, org, dir, count, (float4*)nullptr, occluded);
+}
+
+void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_shade, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, sv, fv, pb, bi,
+                     depth);
+}
+
+void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {
+  hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, pb, depth,
+                     numLights);
+}
+
+void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
+                           uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(k_resolve_pixels, dim3(grid_for(bi.numPixels, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, fv, pb, bi,
+                     fbFloat, fbRGB8, rgb8Stride, accu, accumulate);
+}
+
+void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
+                         uint8_t* fbRGB8, int rgb8Stride, hipStream_t s) {
+  hipLaunchKernelGGL(k_debug, dim3((numTiles + 63) / 64), dim3(64), 0, s, sv, fv, maxDepth, spp, fbFloat, fbRGB8,
+                     rgb8Stride);
+}
+
+}  // namespace yrt

@@ -1,0 +1,354 @@
+// yrt_shade.h — device-side postIntersect, materials, BRDFs and lights.
+//
+// Each function restates the reference's CPU code, keeping the order of the float
+// operations (left-to-right Color*float products etc.) so the GPU and the oracle agree:
+//   postIntersect   shapes/trianglemesh_full.cpp:192-260, trianglemesh_normals.cpp:125-147,
+//                   shapes/triangle.h:69-78
+//   materials       materials/{matte,matte_textured,metallicpaint,obj,Uber,thindielectric}.h
+//   BRDFs           brdfs/{lambertian,dielectric,dielectriclayer,microfacet,specular,
+//                   transmission,optics}.h, brdfs/microfacet/{power_cosine_distribution,fresnel}.h
+//   composition     brdfs/compositedbrdf.h:58-166
+//   lights          lights/{ambientlight,trianglelight}.h, lights/hdrilight.cpp
+//   textures        textures/{Bilinear,nearestneighbor}.h, texel decode
+//                   common/math/color_scalar.h:47 (byte * one_over_255)
+// Omitted reference features (no BASELINE config reaches them): motion blur, participating
+// media (every in-scope material has a vacuum/vacuum interface), metallic-paint glitter,
+// the backplate image; DESIGN.md lists them.
+#pragma once
+
+#include "../common/yrt_gpu_types.h"
+#include "../common/yrt_math.h"
+
+namespace yrt {
+
+// BRDF type bits (brdfs/brdf.h:10-30)
+enum : uint32_t {
+  BT_DIFFUSE = 0x000F000Fu,
+  BT_DIFFUSE_REFLECTION = 0x00000001u,
+  BT_GLOSSY_REFLECTION = 0x00000010u,
+  BT_SPECULAR_REFLECTION = 0x00000100u,
+  BT_SPECULAR_TRANSMISSION = 0x01000000u,
+  BT_TRANSMISSION = 0xFFFF0000u,
+};
+
+enum CompKind : int {
+  C_LAMBERT = 0,          // Lambertian(R)
+  C_DIEL_REFL = 1,        // DielectricReflection(eta_, alpha)          a=eta_, b=alpha
+  C_CONST_DIEL_TRANS = 2, // ConstDielectricTransmission(color)         R=color
+  C_THIN_DIEL_TRANS = 3,  // ThinDielectricTransmission(eta_, logT, th) R=logT, a=eta_, b=thickness
+  C_DIEL_LAYER_LAMB = 4,  // DielectricLayer<Lambertian>(T=1, etait, etati, R)  a=etait, b=etati
+  C_MICROFACET = 5,       // Microfacet<FresnelDielectric(etai,etat),PowerCosine(n,Ns)> R, a=etai, b=etat, c=n
+  C_TRANSMISSION = 6,     // Transmission(T)
+  C_SPECULAR = 7,         // Specular(R, exp)                            a=exp
+};
+
+struct Comp {
+  int kind;
+  uint32_t type;
+  V3 R;
+  float a, b, c;
+};
+
+#define YRT_MAX_COMPS 3
+
+struct BRDFSet {
+  int n;
+  Comp c[YRT_MAX_COMPS];
+};
+
+struct DG {
+  V3 P, Ng, Ns, Tx, Ty;
+  float s, t;   // st
+  float error;
+  int material, light, illumMask, shadowMask;
+};
+
+// ---------------------------------------------------------------- optics
+__device__ __forceinline__ float fresnel3(float cosi, float cost, float eta) {
+  float Rper = (eta * cosi - cost) * rcpf_(eta * cosi + cost);
+  float Rpar = (cosi - eta * cost) * rcpf_(cosi + eta * cost);
+  return 0.5f * (Rpar * Rpar + Rper * Rper);
+}
+__device__ __forceinline__ float fresnel2(float cosi, float eta, float* outCosT) {
+  float k = 1.0f - eta * eta * (1.0f - cosi * cosi);
+  if (k < 0.0f) return 1.0f;
+  float cost = sqrtf(k);
+  if (outCosT) *outCosT = cost;
+  return fresnel3(cosi, cost, eta);
+}
+// refract(V,N,eta,cosi,cost) (brdfs/optics.h:64-70); returns pdf
+__device__ __forceinline__ float refract5(V3 V, V3 N, float eta, float cosi, float& cost, V3& out) {
+  float k = 1.0f - eta * eta * (1.0f - cosi * cosi);
+  if (k < 0.0f) {
+    cost = 0.0f;
+    out = v3s(0.0f);
+    return 0.0f;
+  }
+  cost = sqrtf(k);
+  out = eta * (cosi * N - V) - cost * N;
+  return sqrf(eta);
+}
+__device__ __forceinline__ V3 reflect3(V3 V, V3 N, float cosi) { return 2.0f * cosi * N - V; }
+__device__ __forceinline__ V3 reflect2(V3 V, V3 N) { return reflect3(V, N, dot(V, N)); }
+
+// cosineSampleHemisphere(u,v,N) (samplers/shapesampler.h:80-95)
+__device__ __forceinline__ V3 cosine_hemi(float u, float v, V3 N, float& pdf) {
+  const float phi = kTwoPi * u;
+  const float cosTheta = sqrtf(v), sinTheta = sqrtf(1.0f - v);
+  V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
+  pdf = cosTheta * kOneOverPi;
+  return mul(frame(N), l);
+}
+
+// ---------------------------------------------------------------- textures
+__device__ __forceinline__ void texel(const GpuImage& im, const uint8_t* __restrict__ pool, int x, int y,
+                                      float c[4]) {
+  const float one_over_255 = 1.0f / 255.0f;
+  if (im.format == IMG_RGBAF32) {
+    const float4 f = *(const float4*)(pool + im.offset + ((int64_t)y * im.width + x) * 16);
+    c[0] = f.x; c[1] = f.y; c[2] = f.z; c[3] = f.w;
+    return;
+  }
+  const uint8_t* p = pool + im.offset + ((int64_t)y * im.width + x) * 4;
+  uchar4 b = *(const uchar4*)p;
+  c[0] = b.x * one_over_255;
+  c[1] = b.y * one_over_255;
+  c[2] = b.z * one_over_255;
+  c[3] = im.format == IMG_RGB8 ? 1.0f : b.w * one_over_255;
+}
+
+// Texture::get (textures/Bilinear.h:8-25, textures/nearestneighbor.h:25-32) -> RGBA
+__device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures, const GpuImage* __restrict__ images,
+                                        const uint8_t* __restrict__ pool, int texId, float px, float py,
+                                        float out[4]) {
+  const GpuTexture tx = textures[texId];
+  const GpuImage im = images[tx.image];
+  const float s1 = px - floorf(px), t1 = py - floorf(py);
+  float c[4];
+  if (tx.filter == TEX_BILINEAR) {
+    const float u = s1 * im.width - .5f;
+    const float v = t1 * im.height - .5f;
+    const int x = max(0, min((int)floorf(u), im.width - 2));
+    const int y = max(0, min((int)floorf(v), im.height - 2));
+    const float u_ratio = u - x;
+    const float v_ratio = v - y;
+    const float u_opposite = 1.f - u_ratio;
+    const float v_opposite = 1.f - v_ratio;
+    float c00[4], c10[4], c01[4], c11[4];
+    texel(im, pool, x, y, c00);
+    texel(im, pool, x + 1, y, c10);
+    texel(im, pool, x, y + 1, c01);
+    texel(im, pool, x + 1, y + 1, c11);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      c[k] = (c00[k] * u_opposite + c10[k] * u_ratio) * v_opposite + (c01[k] * u_opposite + c11[k] * u_ratio) * v_ratio;
+  } else {
+    const int si = (int)(s1 * float(im.width)), ti = (int)(t1 * float(im.height));
+    const int ix = max(0, min(si, im.width - 1));
+    const int iy = max(0, min(ti, im.height - 1));
+    texel(im, pool, ix, iy, c);
+  }
+  if (tx.invert) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = 1.f - c[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[k] = c[k];
+}
+
+// ---------------------------------------------------------------- BRDF components
+__device__ __forceinline__ V3 lambert_eval(V3 R, const DG& dg, V3 wi) {
+  return R * kOneOverPi * clampf(dot(wi, dg.Ns));
+}
+
+// Microfacet<FresnelDielectric, PowerCosineDistribution>::eval (brdfs/microfacet.h:28-41)
+__device__ __forceinline__ V3 microfacet_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  if (dot(wi, dg.Ng) <= 0) return v3s(0.0f);
+  const float cosThetaO = dot(wo, dg.Ns);
+  const float cosThetaI = dot(wi, dg.Ns);
+  if (cosThetaI <= 0.0f || cosThetaO <= 0.0f) return v3s(0.0f);
+  const V3 wh = normalize(wi + wo);
+  const float cosThetaH = dot(wh, dg.Ns);
+  const float cosTheta = dot(wi, wh);
+  const float F = fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr);
+  const float n = c.c;
+  const float norm2 = (n + 2) * kOneOverTwoPi;
+  const float D = norm2 * powf(fabsf(dot(wh, dg.Ns)), n);
+  const float G = fminf(fminf(1.0f, 2.0f * cosThetaH * cosThetaO * rcpf_(cosTheta)),
+                        2.0f * cosThetaH * cosThetaI * rcpf_(cosTheta));
+  return c.R * D * G * v3s(F) * rcpf_(4.0f * cosThetaO);
+}
+
+// DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38), T = one
+__device__ __forceinline__ V3 layer_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  float cosThetaO = dot(wo, dg.Ns);
+  float cosThetaI = dot(wi, dg.Ns);
+  if (cosThetaI <= 0.0f || cosThetaO <= 0.0f) return v3s(0.0f);
+  float cosThetaO1, cosThetaI1;
+  V3 wo1, wi1;
+  refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaO1, wo1);
+  refract5(wi, dg.Ns, c.a, cosThetaI, cosThetaI1, wi1);
+  float Fi = 1.0f - fresnel3(cosThetaI, cosThetaI1, c.a);
+  V3 Fg = lambert_eval(c.R, dg, -wi1);
+  float Fo = 1.0f - fresnel3(cosThetaO, cosThetaO1, c.a);
+  return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
+}
+
+__device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  V3 r = reflect2(wo, dg.Ns);
+  if (dot(r, wi) < 0) return v3s(0.0f);
+  return c.R * (c.a + 2) * (1.0f / (2.0f * kPi)) * powf(dot(r, wi), c.a) * clampf(dot(wi, dg.Ns));
+}
+
+__device__ __forceinline__ V3 comp_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  switch (c.kind) {
+    case C_LAMBERT: return lambert_eval(c.R, dg, wi);
+    case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
+    case C_MICROFACET: return microfacet_eval(c, wo, dg, wi);
+    case C_SPECULAR: return specular_eval(c, wo, dg, wi);
+    default: return v3s(0.0f);
+  }
+}
+
+// BRDF::sample of one component; returns color, sets wi/pdf.
+__device__ __forceinline__ V3 comp_sample(const Comp& c, V3 wo, const DG& dg, float sx, float sy, V3& wi,
+                                          float& pdf) {
+  switch (c.kind) {
+    case C_LAMBERT: {
+      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      return lambert_eval(c.R, dg, wi);
+    }
+    case C_DIEL_REFL: {
+      const float cosThetaO = clampf(dot(wo, dg.Ns));
+      wi = reflect3(wo, dg.Ns, cosThetaO);
+      pdf = 1.0f;
+      return c.b * v3s(fresnel2(cosThetaO, c.a, nullptr));
+    }
+    case C_CONST_DIEL_TRANS: {
+      wi = -wo;
+      pdf = 1.0f;
+      const float cosTheta = clampf(dot(wo, dg.Ns));
+      return cosTheta <= 0.0f ? v3s(0.0f) : c.R;
+    }
+    case C_THIN_DIEL_TRANS: {
+      wi = -wo;
+      pdf = 1.0f;
+      const float cosTheta = clampf(dot(wo, dg.Ns));
+      if (cosTheta <= 0.0f) return v3s(0.0f);
+      const float alpha = c.b * rcpf_(cosTheta);
+      float cosThetaT;
+      V3 la = c.R * alpha;
+      return v3(expf(la.x), expf(la.y), expf(la.z)) * (1.f - fresnel2(cosTheta, c.a, &cosThetaT));
+    }
+    case C_DIEL_LAYER_LAMB: {
+      pdf = 0.0f;
+      float cosThetaO = dot(wo, dg.Ns);
+      if (cosThetaO <= 0.0f) return v3s(0.0f);
+      float cosThetaO1;
+      V3 wo1;
+      refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaO1, wo1);
+      float pdf1;
+      V3 wi1 = cosine_hemi(sx, sy, dg.Ns, pdf1);
+      V3 Fg = lambert_eval(c.R, dg, wi1);
+      float cosThetaI1 = dot(wi1, dg.Ns);
+      if (cosThetaI1 <= 0.0f) return v3s(0.0f);
+      float cosThetaI;
+      V3 wi0;
+      float pdf0 = refract5(-wi1, -dg.Ns, c.b, cosThetaI1, cosThetaI, wi0);
+      if (pdf0 == 0.0f) return v3s(0.0f);
+      wi = wi0;
+      pdf = pdf1;
+      float Fi = 1.0f - fresnel3(cosThetaI, cosThetaI1, c.a);
+      float Fo = 1.0f - fresnel3(cosThetaO, cosThetaO1, c.a);
+      return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
+    }
+    case C_MICROFACET: {
+      pdf = 0.0f;
+      if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
+      const float n = c.c;
+      const float norm1 = (n + 1) * kOneOverTwoPi;
+      const float phi = kTwoPi * sx;
+      const float cosPhi = cosf(phi);
+      const float sinPhi = sinf(phi);
+      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float sinTheta = cos2sin(cosTheta);
+      V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+      float whpdf = norm1 * powf(cosTheta, n);
+      wi = reflect2(wo, wh);
+      pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
+      if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
+      return microfacet_eval(c, wo, dg, wi);
+    }
+    case C_TRANSMISSION: {
+      wi = -wo;
+      pdf = 1.0f;
+      return c.R;
+    }
+    case C_SPECULAR: {
+      // powerCosineSampleHemisphere(s.x, s.y, reflect(wo, Ns), exp) (shapesampler.h:104-121)
+      const float e = c.a;
+      const float phi = kTwoPi * sx;
+      const float cosTheta = powf(sy, rcpf_(e + 1));
+      const float sinTheta = cos2sin(cosTheta);
+      V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
+      pdf = (e + 1.0f) * powf(cosTheta, e) * kOneOverTwoPi;
+      wi = mul(frame(reflect2(wo, dg.Ns)), l);
+      return specular_eval(c, wo, dg, wi);
+    }
+  }
+  pdf = 0.0f;
+  return v3s(0.0f);
+}
+
+// CompositedBRDF::eval restricted to `type` (compositedbrdf.h:59-65)
+__device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V3 wi, uint32_t type) {
+  V3 c = v3s(0.0f);
+  for (int i = 0; i < YRT_MAX_COMPS; ++i)
+    if (i < bs.n && (bs.c[i].type & type)) c = c + comp_eval(bs.c[i], wo, dg, wi);
+  return c;
+}
+
+// CompositedBRDF::sample (compositedbrdf.h:104-166)
+__device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg, float sx, float sy, float ss,
+                                         V3& wi_o, float& pdf_o, uint32_t& type_o) {
+  float f[YRT_MAX_COMPS];
+  V3 colors[YRT_MAX_COMPS];
+  V3 dirs[YRT_MAX_COMPS];
+  float pdfs[YRT_MAX_COMPS];
+  uint32_t types[YRT_MAX_COMPS];
+  float sum = 0.0f;
+  int num = 0;
+  for (int i = 0; i < YRT_MAX_COMPS; ++i) {
+    if (i >= bs.n) break;
+    V3 wi;
+    float pdf = 0.0f;
+    V3 c = comp_sample(bs.c[i], wo, dg, sx, sy, wi, pdf);
+    if ((c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) || pdf <= 0.0f) continue;
+    f[num] = (c.x + c.y + c.z) * rcpf_(pdf);
+    sum += f[num];
+    colors[num] = c;
+    dirs[num] = wi;
+    pdfs[num] = pdf;
+    types[num] = bs.c[i].type;
+    num++;
+  }
+  if (num == 0) {
+    wi_o = v3s(0.0f);
+    pdf_o = 0.0f;
+    type_o = 0;
+    return v3s(0.0f);
+  }
+  for (int i = 0; i < num; ++i) f[i] /= sum;
+  float d[YRT_MAX_COMPS];
+  d[0] = f[0];
+  for (int i = 1; i < num - 1; ++i) d[i] = d[i - 1] + f[i];
+  d[num - 1] = 1.0f;
+  int i = 0;
+  while (i < num - 1 && ss > d[i]) i++;
+  wi_o = dirs[i];
+  pdf_o = pdfs[i] * f[i];
+  type_o = types[i];
+  return colors[i];
+}
+
+}  // namespace yrt
