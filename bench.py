@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s (+ samples/s) of the MI355X wavefront path tracer on the
+BASELINE.json C3 workload — Sponza-class atrium stand-in (yrt.standin, seed 1234, 67 k tris,
+Uber + Sponza JPEG textures, dome light 8 8 8), 2048x2048, 64 spp, depth 10,
+tMaxShadowRay 120, camera of models/test_stereo_view.ecs:2-10.
+
+One step = one full frame (all W*H*spp paths to termination) rendered through the C ABI
+(yrtRenderFrame), scene resident in HBM. With N GPUs (torch.distributed, one process per
+GPU) the frame's 16x16 tiles are dealt round-robin over the ranks, each rank
+renders its shard, and the RGB8 shards are combined on rank 0 with one RCCL reduce
+(disjoint supports, so the sum is a gather) inside the step.
+
+Weak scaling: at N GPUs one step is N progressive iterations of that frame (AccuBuffer
+accumulation, integratorrenderer.cpp:166), all tiles of all N iterations dealt round-robin;
+per-GPU work stays one C3 frame. N=1 is exactly C3.
+
+Counting: rays = closest-hit + shadow queries (numRays of
+pathtraceintegrator.cpp:74,161); Mrays/s = rays of all ranks / max-over-ranks wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "yulio-raytracer_amd"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md §HBM
+NODE_BYTES, TRI_BYTES = 64, 48  # GpuNode / GpuTri (csrc/common/yrt_gpu_types.h)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--size", type=int, default=2048)
+    p.add_argument("--spp", type=int, default=64)
+    p.add_argument("--cpu-rows", type=int, default=48, help="rows of the centred CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import yrt
+    from yrt import standin
+    xml = ROOT / "scenes" / "_generated" / f"sponza_standin_r{rank}.xml"
+    standin.write_xml(xml)
+    dev = yrt.Device(local)
+    args = ["-i", str(xml)] + standin.C3_ARGS + ["-size", str(a.size), str(a.size), "-spp", str(a.spp)]
+    ses = yrt.Session(args, device=dev)
+    info = ses.info()
+    cam = ses.camera()
+    R, S, T, F = info["renderer"], info["scene"], info["tonemapper"], info["framebuffer"]
+    sinfo = dev.scene_info(S)
+    dev.set_tile_shard(rank, world)
+
+    # ---- untimed capture frame: visit counts of the real query streams (roofline bytes)
+    import oracle
+    dev.set_ray_capture(a.capture)
+    dev.rtRenderFrame(R, cam, S, T, F, 0)
+    dev.set_ray_capture(0)
+    nodes, tris = dev.export_bvh(S)
+    per_kind = {}
+    for shadow in (0, 1):
+        tot_rays = tot_nodes = tot_tris = 0.0
+        for depth in range(64):
+            org, dr, total = dev.captured_rays(shadow, depth)
+            if len(org):
+                nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow))
+                tot_rays += total
+                tot_nodes += nv / len(org) * total
+                tot_tris += tv / len(org) * total
+        n_node = tot_nodes / max(tot_rays, 1)
+        n_tri = tot_tris / max(tot_rays, 1)
+        io = 32 + (4 if shadow else 16)
+        per_kind["shadow" if shadow else "closest"] = {
+            "nodes_per_ray": n_node, "tris_per_ray": n_tri,
+            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * TRI_BYTES}
+
+    # ---- warmup + timed frames
+    dev.set_kernel_timing(True)
+    fb_t = None
+    if world > 1:
+        stride = (3 * a.size + 3) // 4 * 4
+        fb_t = torch.empty(stride * a.size, dtype=torch.uint8, device="cuda")
+
+    def step():
+        # weak scaling: the job is `world` progressive iterations of the C3 frame (sampler
+        # iteration k = frame k); every frame's tiles are dealt round-robin over the ranks,
+        # so each rank renders one frame's worth of tiles per step.
+        st = None
+        for k in range(world):
+            dev.rtRenderFrame(R, cam, S, T, F, 1 if k else 0)
+            s_k = dev.render_stats()
+            st = s_k if st is None else {n: st[n] + s_k[n] for n in st}
+        if world > 1:
+            import ctypes
+            p = dev.rtMapFrameBuffer(F)
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * fb_t.numel()).from_address(p))
+            fb_t.copy_(torch.from_numpy(host), non_blocking=False)
+            dev.rtUnmapFrameBuffer(F)
+            dist.reduce(fb_t, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = {"rays": 0.0, "closest": 0.0, "shadow": 0.0, "samples": 0.0, "msClosest": 0.0, "msShadow": 0.0,
+           "msShade": 0.0, "nClosest": 0.0, "nShadow": 0.0}
+    for _ in range(a.steps):
+        st = step()
+        acc["closest"] += st["raysClosest"]
+        acc["shadow"] += st["raysShadow"]
+        acc["rays"] += st["raysClosest"] + st["raysShadow"]
+        acc["msClosest"] += st["msTraceClosest"]
+        acc["msShadow"] += st["msTraceShadow"]
+        acc["msShade"] += st["msShade"]
+        acc["nClosest"] += st["launchesClosest"]
+        acc["nShadow"] += st["launchesShadow"]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    samples_total = float(a.size) * a.size * 2 ** int(np.ceil(np.log2(a.spp))) * a.steps * world
+
+    tot = torch.tensor([acc["rays"], acc["closest"], acc["shadow"]], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    rays, closest, shadow = tot.tolist()
+    elapsed = tmax.item()
+
+    if rank == 0:
+        # dominant trace kernel and its roofline (algorithmic bytes / kernel time)
+        kern = {
+            "closest": (acc["msClosest"], acc["closest"], acc["nClosest"]),
+            "shadow": (acc["msShadow"], acc["shadow"], acc["nShadow"]),
+        }
+        dom = max(kern, key=lambda k: kern[k][0])
+        ms, nr, nl = kern[dom]
+        bytes_total = nr * per_kind[dom]["bytes_per_ray"]
+        achieved = bytes_total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_trace_closest" if dom == "closest" else "k_trace_any",
+                "launches": int(nl), "avg_launch_ms": round(ms / max(nl, 1), 4),
+                "algorithmic_bytes_per_launch": round(bytes_total / max(nl, 1)),
+                "visits": per_kind,
+                "kernel_ms_per_step": {"trace_closest": acc["msClosest"] / a.steps,
+                                       "trace_shadow": acc["msShadow"] / a.steps,
+                                       "shade": acc["msShade"] / a.steps}}
+        cpu = None
+        if not a.no_cpu_baseline:
+            cpu = cpu_baseline(ses, a)
+        out = {
+            "metric": "Mrays/s (Sponza stand-in 2048^2 64spp, closest+shadow queries)",
+            "value": round(rays / elapsed / 1e6, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural Sponza-class atrium, seed 1234; Sponza.DAE absent)",
+            "config": {"workload": "C3 sponza_standin 2048x2048 64spp depth10 dome(8,8,8) tMaxShadowRay120",
+                       "width": a.size, "height": a.size, "spp": a.spp, "triangles": sinfo["numTriangles"],
+                       "bvh_nodes": sinfo["numNodes"], "parallelism": f"tiles-roundrobin{world}"},
+            "samples_per_s": round(samples_total / elapsed, 1),
+            "rays_closest": closest, "rays_shadow": shadow,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ses.close()
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ses, a):
+    """The oracle (CPU restatement of the reference path) on a bounded, centred band of the
+    same frame: a.cpu_rows rows x full width, same spp/depth/scene/camera."""
+    import oracle
+    blob = ses.export_frame()
+    threads = min(16, oracle.cpu_count())
+    y0 = (a.size - a.cpu_rows) // 2
+    t = time.perf_counter()
+    _, st = oracle.render(blob, a.size, a.size, ses.info()["gamma"], rect=(0, y0, a.size, y0 + a.cpu_rows),
+                          threads=threads)
+    dt = time.perf_counter() - t
+    rays = st["raysClosest"] + st["raysShadow"]
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"rows [{y0},{y0 + a.cpu_rows}) x {a.size} px at {a.spp} spp of the same frame "
+                      f"({rays:.0f} rays in {dt:.1f} s)",
+            "samples_per_s": round(st["samples"] / dt, 1)}
+
+
+if __name__ == "__main__":
+    main()

@@ -149,6 +149,17 @@ YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
 YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
 /* Host sampler check: writes the SoA sample table (dims x (sets*spp)) that the frame
  * renderer uploads (sampler/sampler.cpp:46-126 restated); returns sets*spp records. */
+/* Ray capture for the roofline's algorithmic bytes: while maxPerDepth > 0,
+ * yrtRenderFrame keeps a strided sample (<= maxPerDepth rays) of the closest-hit and shadow
+ * query streams of every depth of its first wavefront batch (synchronizes per depth: use on
+ * an untimed frame). yrtGetCapturedRays returns the sample size and the stream's full size. */
+YRT_API int yrtSetRayCapture(YRTDevice dev, int maxPerDepth);
+YRT_API int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* org4, float* dir4, size_t maxRays,
+                                   double* totalInBatch);
+/* Decoder check: 8-bit pixels of a .jpg/.png in file row order (top row first), before the
+ * Image4c flip/requantization of rtNewImageFromFile. Call with out=NULL to get the size. */
+YRT_API int yrtDebugDecodeImage(const char* file, int* width, int* height, int* channels, uint8_t* out,
+                                size_t outBytes);
 YRT_API int yrtDebugSampleTable(int spp, int sets, int iteration, int num1D, int num2D, const char* filter,
                                 float* out, size_t outFloats);
 

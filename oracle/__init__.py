@@ -1,0 +1,126 @@
+"""ctypes wrapper of liboracle.so — the CPU restatement of the reference render path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker. The product (yulio-raytracer_amd/) never imports it.
+See yrt_oracle.h for what it restates (reference file:line) and its documented substitutions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-C", str(HERE)], check=True, stdout=subprocess.DEVNULL)
+
+
+if not LIB.exists():
+    build()
+_lib = C.CDLL(str(LIB))
+
+vp, sz, i32, PF = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_float)
+
+
+class OracleStats(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("raysClosest", "raysShadow", "samples", "seconds", "nodeVisits",
+                                          "triVisits")]
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype, f.argtypes = res, list(args)
+
+
+_sig("oracle_render", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, vp, C.POINTER(OracleStats))
+_sig("oracle_trace", i32, vp, sz, vp, vp, i32, i32, vp)
+_sig("oracle_count_visits", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
+     C.POINTER(C.c_double), vp)
+_sig("oracle_random_ints", None, i32, i32, vp)
+_sig("oracle_sample_table", i32, i32, i32, i32, i32, i32, C.c_char_p, vp, sz)
+_sig("oracle_pixel_sets", None, i32, i32, i32, vp)
+_sig("oracle_scene_triangles", i32, vp, sz, vp, i32)
+_sig("oracle_last_error", C.c_char_p)
+
+
+def _err():
+    e = _lib.oracle_last_error()
+    return e.decode() if e else "?"
+
+
+def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0):
+    """RGB_FLOAT32 image (H, W, 3) of the frame blob; pixels outside rect stay NaN."""
+    x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
+    out = np.full((height, width, 3), np.nan, np.float32)
+    st = OracleStats()
+    rc = _lib.oracle_render(blob, len(blob), width, height, gamma, x0, y0, x1, y1, threads, out.ctypes.data,
+                            C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render: {_err()}")
+    return out, {n: getattr(st, n) for n, _ in st._fields_}
+
+
+def trace(blob: bytes, org4: np.ndarray, dir4: np.ndarray, any_hit=False):
+    org4 = np.ascontiguousarray(org4, np.float32)
+    dir4 = np.ascontiguousarray(dir4, np.float32)
+    n = org4.shape[0]
+    hit = np.zeros((n, 4), np.float32)
+    rc = _lib.oracle_trace(blob, len(blob), org4.ctypes.data, dir4.ctypes.data, n, int(any_hit), hit.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle_trace: {_err()}")
+    return hit
+
+
+def count_visits(nodes: np.ndarray, tris: np.ndarray, org4, dir4, any_hit=False):
+    org4 = np.ascontiguousarray(org4, np.float32)
+    dir4 = np.ascontiguousarray(dir4, np.float32)
+    n = org4.shape[0]
+    nv, tv = C.c_double(), C.c_double()
+    hit = np.zeros((n, 4), np.float32)
+    rc = _lib.oracle_count_visits(nodes.ctypes.data, nodes.nbytes // 64, tris.ctypes.data, tris.nbytes // 48,
+                                  org4.ctypes.data, dir4.ctypes.data, n, int(any_hit), C.byref(nv), C.byref(tv),
+                                  hit.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle_count_visits: {_err()}")
+    return nv.value, tv.value, hit
+
+
+def random_ints(seed, n):
+    out = np.zeros(n, np.int32)
+    _lib.oracle_random_ints(seed, n, out.ctypes.data)
+    return out
+
+
+def sample_table(spp, sets, iteration, num1D, num2D, filter="bspline"):
+    n = _lib.oracle_sample_table(spp, sets, iteration, num1D, num2D, filter.encode(), None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle_sample_table: {_err()}")
+    dims = 5 + num1D + 2 * num2D
+    out = np.zeros(dims * n, np.float32)
+    _lib.oracle_sample_table(spp, sets, iteration, num1D, num2D, filter.encode(), out.ctypes.data, out.size)
+    return out.reshape(dims, n)
+
+
+def pixel_sets(width, height, sets):
+    out = np.zeros(width * height, np.uint8)
+    _lib.oracle_pixel_sets(width, height, sets, out.ctypes.data)
+    return out.reshape(height, width)
+
+
+def scene_triangles(blob: bytes):
+    n = _lib.oracle_scene_triangles(blob, len(blob), None, 0)
+    if n < 0:
+        raise RuntimeError(f"oracle_scene_triangles: {_err()}")
+    out = np.zeros((n, 9), np.float32)
+    _lib.oracle_scene_triangles(blob, len(blob), out.ctypes.data, n)
+    return out
+
+
+def cpu_count():
+    return len(os.sched_getaffinity(0))

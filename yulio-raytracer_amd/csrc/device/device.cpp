@@ -46,6 +46,26 @@ class Device {
   int shardIndex = 0, shardCount = 1;
   bool kernelTiming = false;
   YRTRenderStats stats{};
+  // ray capture (roofline accounting): strided sample of each depth's query streams, batch 0
+  int captureMax = 0;
+  struct Captured { std::vector<float> org, dir; double total = 0; };
+  std::vector<Captured> capClosest, capShadow;
+  void capture(std::vector<Captured>& out, int depth, const float4* org, const float4* dir, const unsigned* dcount) {
+    unsigned n = 0;
+    HIP_CHECK(hipMemcpyAsync(&n, dcount, sizeof(n), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    if ((int)out.size() <= depth) out.resize(depth + 1);
+    Captured& c = out[depth];
+    c.total = n;
+    const size_t stride = std::max<size_t>(1, (n + captureMax - 1) / captureMax);
+    const size_t m = n ? (n + stride - 1) / stride : 0;
+    c.org.resize(m * 4);
+    c.dir.resize(m * 4);
+    if (m) {
+      HIP_CHECK(hipMemcpy2D(c.org.data(), 16, org, stride * 16, 16, m, hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy2D(c.dir.data(), 16, dir, stride * 16, 16, m, hipMemcpyDeviceToHost));
+    }
+  }
 
   // per-frame device state
   DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCounters, dCount;
@@ -195,6 +215,10 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
   dFbFloat.alloc((size_t)W * H * 3 * sizeof(float));
   dFbRGB8.alloc(rgb8Stride * H);
+  if (shardCount > 1) {  // pixels of other shards stay 0 so per-rank images compose by sum
+    HIP_CHECK(hipMemsetAsync(dFbFloat.p, 0, (size_t)W * H * 3 * sizeof(float), stream));
+    HIP_CHECK(hipMemsetAsync(dFbRGB8.p, 0, rgb8Stride * H, stream));
+  }
 
   FrameView fv;
   fv.rp = dRp.as<GpuRenderParams>();
@@ -216,6 +240,8 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     stats.raysClosest = 0;
   } else {
     launch_pixel_sets(fv, dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
+    capClosest.clear();
+    capShadow.clear();
     const int spp = rp.spp;
     int64_t tilesPerBatch = std::max<int64_t>(1, capacity / (256ll * spp));
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
@@ -260,6 +286,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, stream)); }
         launch_trace_closest(G.view, pb.qOrg[cur], pb.qDir[cur], pb.counters + d * 4, pb.capacity, pb.hit, stream);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, stream)); evs.push_back(e1); }
+        if (captureMax > 0 && first == 0) capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + d * 4);
         EvPair e2{};
         if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
         launch_shade(G.view, fv, pb, bi, d, stream);
@@ -269,6 +296,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
           launch_trace_any(G.view, pb.sOrg, pb.sDir, pb.counters + d * 4 + 1, pb.shadowCapacity, pb.sOcc, stream);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
+          if (captureMax > 0 && first == 0) capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + d * 4 + 1);
           launch_shadow_resolve(pb, d, rp.numLights, stream);
         }
       }
@@ -865,6 +893,63 @@ int yrtDebugSampleTable(int spp, int sets, int iteration, int num1D, int num2D, 
   } catch (...) {
     return -1;
   }
+}
+
+int yrtDebugDecodeImage(const char* file, int* width, int* height, int* channels, uint8_t* out, size_t outBytes) {
+  try {
+    FILE* f = fopen(file, "rb");
+    if (!f) return -1;
+    std::vector<uint8_t> bytes;
+    uint8_t buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof(buf), f)) > 0) bytes.insert(bytes.end(), buf, buf + n);
+    fclose(f);
+    std::string err;
+    std::vector<uint8_t> px;
+    int w = 0, h = 0, c = 3;
+    const char* dot = strrchr(file, '.');
+    if (dot && (!strcasecmp(dot, ".jpg") || !strcasecmp(dot, ".jpeg"))) {
+      if (!decode_jpeg(bytes, w, h, px, err)) return -2;
+    } else if (dot && !strcasecmp(dot, ".png")) {
+      if (!decode_png(bytes, w, h, c, px, err)) return -2;
+    } else {
+      return -3;
+    }
+    *width = w;
+    *height = h;
+    *channels = c;
+    if (out && outBytes >= px.size()) memcpy(out, px.data(), px.size());
+    return 0;
+  } catch (...) {
+    return -4;
+  }
+}
+
+int yrtSetRayCapture(YRTDevice dev, int maxPerDepth) {
+  DEV_GUARD(dev, -1)
+  dev->d->captureMax = std::max(0, maxPerDepth);
+  return 0;
+  DEV_END(-1)
+}
+
+int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* org4, float* dir4, size_t maxRays,
+                           double* totalInBatch) {
+  DEV_GUARD(dev, -1)
+  auto& v = shadow ? dev->d->capShadow : dev->d->capClosest;
+  if (depth < 0 || depth >= (int)v.size()) {
+    if (totalInBatch) *totalInBatch = 0;
+    return 0;
+  }
+  const auto& c = v[depth];
+  const size_t m = c.org.size() / 4;
+  if (totalInBatch) *totalInBatch = c.total;
+  if (org4 && dir4) {
+    const size_t k = std::min(m, maxRays);
+    memcpy(org4, c.org.data(), k * 16);
+    memcpy(dir4, c.dir.data(), k * 16);
+  }
+  return (int64_t)m;
+  DEV_END(-1)
 }
 
 int yrtSetTileShard(YRTDevice dev, int index, int count) {
