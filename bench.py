@@ -62,6 +62,7 @@ def main():
 
     import yrt
     from yrt import standin
+    from yrt.dist import gather_frame
     xml = ROOT / "scenes" / "_generated" / f"sponza_standin_r{rank}.xml"
     standin.write_xml(xml)
     dev = yrt.Device(local)
@@ -118,7 +119,7 @@ def main():
             host = np.ctypeslib.as_array((ctypes.c_uint8 * fb_t.numel()).from_address(p))
             fb_t.copy_(torch.from_numpy(host), non_blocking=False)
             dev.rtUnmapFrameBuffer(F)
-            dist.reduce(fb_t, dst=0, op=dist.ReduceOp.SUM)
+            gather_frame(fb_t, dst=0)
         return st
 
     for _ in range(a.warmup):

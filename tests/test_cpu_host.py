@@ -1,0 +1,290 @@
+"""CPU suite: oracle against golden vectors, host logic of the device plugin (loaders, BVH,
+sampler, decoders, frame export) and the C-ABI surface. No GPU calls."""
+import ctypes
+import json
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import yrt
+from helpers import ROOT, SCENES, c1_args, c2_args, c3_args, c4_args
+
+GOLDEN = ROOT / "tests" / "golden"
+
+
+# ----------------------------------------------------------------------------- Random (KAT 1)
+def _random_ref(seed, n):
+    """Independent restatement of embree::Random (common/math/random.h:31-65): Park-Miller
+    minimal standard with a 32-entry Bays-Durham shuffle, 32-bit signed arithmetic."""
+    a, m, q, r = 16807, 2147483647, 127773, 2836
+    s = 1 if seed == 0 else (-seed if seed < 0 else seed)
+    table = [0] * 32
+    for j in range(39, -1, -1):
+        k = int(s / q)
+        s = a * (s - k * q) - r * k
+        if s < 0:
+            s += m
+        if j < 32:
+            table[j] = s
+    state = table[0]
+    out = []
+    for _ in range(n):
+        k = int(s / q)
+        s = a * (s - k * q) - r * k
+        if s < 0:
+            s += m
+        j = state // (1 + (2147483647 - 1) // 32)
+        state = table[j]
+        table[j] = s
+        out.append(state)
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1, 27, 3433, 81551, 91711, 91711 * 5 + 81551 * 3])
+def test_random_matches_restatement(seed):
+    assert oracle.random_ints(seed, 200).tolist() == _random_ref(seed, 200)
+
+
+def test_random_golden():
+    g = json.loads((GOLDEN / "random_ints.json").read_text())
+    for seed, vals in g.items():
+        assert oracle.random_ints(int(seed), len(vals)).tolist() == vals
+
+
+# ----------------------------------------------------------------------------- sampler (KAT 2)
+@pytest.mark.parametrize("spp,depth", [(1, 2), (16, 2), (64, 10), (3, 4)])
+def test_sample_table_host_equals_oracle(spp, depth):
+    """Product host sampler (csrc/device/sampler.cpp) vs oracle restatement: bit-exact."""
+    a = yrt.sample_table(spp, 64, 0, depth, depth + 1)
+    b = oracle.sample_table(spp, 64, 0, depth, depth + 1)
+    assert a.shape == b.shape
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("spp,depth", [(1, 2), (16, 2), (64, 10)])
+def test_sample_table_golden(spp, depth):
+    g = np.load(GOLDEN / f"sample_table_spp{spp}_d{depth}.npy")
+    b = oracle.sample_table(spp, 64, 0, depth, depth + 1)
+    assert np.array_equal(g, b)
+
+
+def test_sample_table_spp_rounds_up_to_pow2():
+    """Quirk Q5 (samplers/sampler.cpp:91): spp is rounded up to a power of two."""
+    assert yrt.sample_table(3, 64, 0, 1, 2).shape[1] == 4 * 64
+    assert yrt.sample_table(33, 8, 0, 1, 2).shape[1] == 64 * 8
+
+
+def test_pixel_sets_golden():
+    g = np.load(GOLDEN / "pixel_sets_100x70.npy")
+    assert np.array_equal(oracle.pixel_sets(100, 70, 64), g)
+
+
+# ----------------------------------------------------------------------------- decoders
+@pytest.mark.parametrize("name", sorted(p.name for p in (SCENES / "Sponza").glob("*.JPG")) + ["../logo.png"])
+def test_image_decoders_match_pil(name):
+    """Baseline JPEG (islow IDCT, fancy upsampling) and PNG decoders vs libjpeg-turbo/zlib via PIL."""
+    PIL = pytest.importorskip("PIL.Image")
+    f = SCENES / "Sponza" / name
+    a = yrt.decode_image(f)
+    b = np.asarray(PIL.open(f))
+    if b.ndim == 2:
+        b = b[..., None]
+    assert a.shape == b.shape and np.array_equal(a, b)
+
+
+# ----------------------------------------------------------------------------- loaders + commit
+@pytest.mark.parametrize("args,tris,lights", [
+    (c1_args(32), 36, 2),           # 34 OBJ triangles + quad light (2 triangle lights)
+    (c2_args(32, 1), 2 * 4900 + 10 + 2, 2),
+    (c4_args(32, 1, stereo=False), 3 * 4900 + 2 + 2, 2),
+])
+def test_scene_load_counts(host_device, args, tris, lights):
+    s = yrt.Session(args, device=host_device)
+    info = host_device.scene_info(s.info()["scene"])
+    assert info["numTriangles"] == tris
+    assert info["numLights"] == lights
+    s.close()
+
+
+def test_standin_is_deterministic_and_sized():
+    from yrt import standin
+    a = [m.arrays() for m in standin.build_meshes()]
+    b = [m.arrays() for m in standin.build_meshes()]
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert (u is None and v is None) or np.array_equal(u, v)
+    n = sum(x[3].shape[0] for x in a)
+    assert 60000 <= n <= 70000
+
+
+def _incoherent(blob, n, seed=42):
+    tris = oracle.scene_triangles(blob).reshape(-1, 3, 3)
+    lo, hi = tris.min(axis=(0, 1)), tris.max(axis=(0, 1))
+    rng = np.random.default_rng(seed)
+    org = rng.uniform(lo, hi, size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    org4 = np.concatenate([org, np.zeros((n, 1))], 1).astype(np.float32)
+    dir4 = np.concatenate([d, np.full((n, 1), np.inf)], 1).astype(np.float32)
+    return org4, dir4
+
+
+@pytest.mark.parametrize("which", ["C1", "C2", "C3", "C4"])
+def test_device_bvh_gives_oracle_hits(host_device, which):
+    """The product's SAH BVH (csrc/device/bvh_build.cpp), traversed in the device kernel's
+    order by the oracle, returns the same closest hits as the oracle's own BVH: the
+    (t, triangle id) tie-break makes the hit independent of the tree."""
+    args = {"C1": c1_args(32), "C2": c2_args(32, 1), "C3": c3_args(32, 1),
+            "C4": c4_args(32, 1, stereo=False)}[which]
+    s = yrt.Session(args, device=host_device)
+    scene = s.info()["scene"]
+    blob = s.export_frame()
+    nodes, tris = host_device.export_bvh(scene)
+    org4, dir4 = _incoherent(blob, 4096)
+    ref = oracle.trace(blob, org4, dir4)
+    nv, tv, hit = oracle.count_visits(nodes, tris, org4, dir4)
+    assert np.array_equal(hit[:, 3].view(np.int32), ref[:, 3].view(np.int32))
+    m = ref[:, 3].view(np.int32) >= 0
+    assert np.array_equal(hit[m, :3], ref[m, :3])
+    assert nv > 0 and tv > 0
+    s.close()
+
+
+def test_bvh_depth_within_stack(host_device):
+    s = yrt.Session(c3_args(32, 1), device=host_device)
+    info = host_device.scene_info(s.info()["scene"])
+    assert info["bvhDepth"] <= 39  # YRT_STACK_DEPTH - 1
+    s.close()
+
+
+def test_export_frame_deterministic(host_device):
+    s1 = yrt.Session(c2_args(32, 1), device=host_device)
+    s2 = yrt.Session(c2_args(32, 1), device=host_device)
+    assert s1.export_frame() == s2.export_frame()
+    s1.close()
+    s2.close()
+
+
+# ----------------------------------------------------------------------------- oracle goldens
+@pytest.mark.parametrize("name,args", [
+    ("c1_64", c1_args(64, 1)), ("c2_64", c2_args(64, 4)), ("c4_face3_64", c4_args(64, 4)),
+])
+def test_oracle_thumbnails_golden(host_device, name, args):
+    """Oracle 64x64 thumbnails (KAT 6) stay bit-identical to the committed fixtures."""
+    g = np.load(GOLDEN / f"thumb_{name}.npy")
+    face = 3 if "face3" in name else -1
+    s = yrt.Session(args + ["-fb", "RGB_FLOAT32"], device=host_device)
+    img, _ = oracle.render(s.export_frame(face), 64, 64, s.info()["gamma"])
+    assert np.array_equal(img, g)
+    s.close()
+
+
+def test_oracle_debug_renderer_golden(host_device):
+    g = np.load(GOLDEN / "debug_c2_64.npy")
+    s = yrt.Session(c2_args(64, 1) + ["-renderer", "debug", "-fb", "RGB_FLOAT32"], device=host_device)
+    img, _ = oracle.render(s.export_frame(), 64, 64, 1.0)
+    assert np.array_equal(img, g)
+    s.close()
+
+
+def test_white_furnace(host_device):
+    """KAT 5: an open Lambertian plane under a constant dome with nothing above it: every
+    primary hit returns the dome radiance times the albedo (one diffuse vertex)."""
+    d = host_device
+    L, albedo = 2.0, 0.5
+    mesh = d.rtNewShape("trianglemesh")
+    pos = np.array([[-1e3, 0, -1e3], [1e3, 0, -1e3], [1e3, 0, 1e3], [-1e3, 0, 1e3]], np.float32)
+    idx = np.array([[0, 2, 1], [0, 3, 2]], np.int32)
+    dp, di = d.rtNewData("immutable", pos), d.rtNewData("immutable", idx)
+    d.rtSetArray(mesh, "positions", "float3", dp, 4, 12)
+    d.rtSetArray(mesh, "indices", "int3", di, 2, 12)
+    d.rtCommit(mesh)
+    mat = d.rtNewMaterial("Matte")
+    d.rtSetFloat3(mat, "reflectance", albedo, albedo, albedo)
+    d.rtCommit(mat)
+    amb = d.rtNewLight("ambientlight")
+    d.rtSetFloat3(amb, "L", L, L, L)
+    d.rtCommit(amb)
+    scene = d.rtNewScene("default")
+    d.rtSetPrimitive(scene, 0, d.rtNewShapePrimitive(mesh, mat))
+    d.rtSetPrimitive(scene, 1, d.rtNewLightPrimitive(amb))
+    d.rtCommit(scene)
+    cam = d.rtNewCamera("pinhole")
+    d.rtSetTransform(cam, "local2world", yrt_lookat((0, 10, 0), (0, 10, 1), (0, 1, 0)))
+    d.rtSetFloat1(cam, "angle", 60.0)
+    d.rtSetFloat1(cam, "aspectRatio", 1.0)
+    d.rtCommit(cam)
+    r = d.rtNewRenderer("pathtracer")
+    d.rtSetInt1(r, "maxDepth", 2)
+    d.rtSetInt1(r, "sampler.spp", 4)
+    d.rtSetFloat1(r, "tMaxShadowRay", 1e4)
+    d.rtCommit(r)
+    blob = d.export_frame(r, cam, scene)
+    img, _ = oracle.render(blob, 32, 32, 1.0)
+    # every pixel sees either the dome (L) or the plane (L * albedo); filter-blended horizon
+    # pixels lie in between
+    plane = np.isclose(img, L * albedo, rtol=2e-3)
+    sky = np.isclose(img, L, rtol=2e-3)
+    assert plane.mean() > 0.3 and sky.mean() > 0.3, (plane.mean(), sky.mean())
+    assert (img >= L * albedo * (1 - 2e-3)).all() and (img <= L * (1 + 2e-3)).all()
+
+
+def yrt_lookat(eye, point, up):
+    """lookAtPoint (common/math/affinespace.h:72-77) as the 12-float rtSetTransform layout."""
+    eye, point, up = (np.asarray(v, np.float64) for v in (eye, point, up))
+    z = point - eye
+    z /= np.linalg.norm(z)
+    u = np.cross(up, z)
+    u /= np.linalg.norm(u)
+    v = np.cross(z, u)
+    v /= np.linalg.norm(v)
+    return np.concatenate([u, v, z, eye]).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- C-ABI surface
+def _declared(header):
+    txt = (ROOT / "include" / header).read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = "\n".join(l for l in txt.splitlines() if not l.lstrip().startswith("#"))
+    names = re.findall(r"(?:YRT_API|YULIO_DLL_EXPORT)[^;(]*?\b(\w+)\s*\(", txt)
+    return sorted(set(names))
+
+
+@pytest.mark.parametrize("header,lib", [("yrt_device.h", "dev"), ("yrt_frontend.h", "fe"), ("YulioRT.h", "fe")])
+def test_every_declared_symbol_is_exported(header, lib):
+    from yrt import _native
+    so = getattr(_native, lib)
+    names = _declared(header)
+    assert len(names) >= 5
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_host_device_refuses_rendering(host_device):
+    s = yrt.Session(c1_args(16), device=host_device)
+    with pytest.raises(RuntimeError, match="host-only"):
+        s.render()
+    s.close()
+
+
+def test_out_of_scope_types_fail_loudly(host_device):
+    with pytest.raises(RuntimeError, match="scope"):
+        host_device.rtNewMaterial("Velvet")
+    with pytest.raises(RuntimeError):
+        host_device.rtNewLight("pointlight")
+
+
+def test_params_rt_defaults():
+    """InitParamsRT fills the YulioRT.h:37-50 defaults."""
+    p = yrt.InitParamsRT()
+    assert p.renderer == b"pathtracer" and p.size == 1536 and p.depth == 10 and p.spp == 256
+    assert abs(p.tMaxShadowRay - 120.0) < 1e-6 and p.toeIn and not p.waterMark
+    assert list(p.ambientlight) == pytest.approx([0.83, 0.95, 0.98])
+    assert p.faceCullingMode == b"default"
+
+
+def test_start_rt_rejects_missing_and_collada(tmp_path):
+    assert not yrt.StartRT(tmp_path / "x.txt")
+    assert yrt.GetLastErrorRT() == 2  # MissingColladaFile

@@ -120,6 +120,9 @@ def test_tile_shards_compose_bit_exact(gpu_device):
         gpu_device.set_tile_shard(k, 3)
         parts.append(s.render())
     gpu_device.set_tile_shard(0, 1)
+    from yrt.dist import tile_mask
+    for k, p in enumerate(parts):
+        assert not p[~tile_mask(200, 200, k, 3)].any()
     assert np.array_equal(sum(parts), full)
     s.close()
 
