@@ -46,6 +46,8 @@ YRT_API const char* yrtGetLastError(YRTDevice dev);
 /* ---- object creation (device.h:126-214) ---------------------------------------------- */
 YRT_API YRTHandle yrtNewCamera(YRTDevice dev, const char* type);        /* "pinhole", "stereo" */
 YRT_API YRTHandle yrtNewData(YRTDevice dev, const char* type, size_t bytes, const void* data);
+/* rtNewDataFromFile (device.h:144, singleray_device.cpp:204-222): "immutable" only. */
+YRT_API YRTHandle yrtNewDataFromFile(YRTDevice dev, const char* type, const char* file, size_t offset, size_t bytes);
 YRT_API YRTHandle yrtNewImage(YRTDevice dev, const char* type, size_t width, size_t height, const void* data);
                                                                        /* "RGB8","RGBA8","RGB_FLOAT32","RGBA_FLOAT32" */
 YRT_API YRTHandle yrtNewImageFromFile(YRTDevice dev, const char* file); /* .ppm/.png/.jpg */
@@ -56,8 +58,15 @@ YRT_API YRTHandle yrtNewLight(YRTDevice dev, const char* type);         /* "ambi
 YRT_API YRTHandle yrtNewShapePrimitive(YRTDevice dev, YRTHandle shape, YRTHandle material, const float* transform12,
                                        int faceCamera);
 YRT_API YRTHandle yrtNewLightPrimitive(YRTDevice dev, YRTHandle light, YRTHandle material, const float* transform12);
+/* rtTransformPrimitive (device.h:197): new primitive with transform * prim.transform. */
+YRT_API YRTHandle yrtTransformPrimitive(YRTDevice dev, YRTHandle prim, const float* transform12);
 YRT_API YRTHandle yrtNewScene(YRTDevice dev, const char* type);
 YRT_API int yrtSetPrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim);
+/* rtUpdatePrimitive (device.h:207, singleray_device.cpp:354-398): re-aims a faceCamera
+ * primitive at camPos (floor-projected) with up camUp; no-op for other primitives. The scene
+ * must be re-committed afterwards, as renderer.cpp:550-559 does per cube face. */
+YRT_API int yrtUpdatePrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim, const float* camPos3,
+                               const float* camUp3);
 YRT_API YRTHandle yrtNewToneMapper(YRTDevice dev, const char* type);    /* "default" */
 YRT_API YRTHandle yrtNewRenderer(YRTDevice dev, const char* type);      /* "pathtracer", "debug" */
 YRT_API YRTHandle yrtNewFrameBuffer(YRTDevice dev, const char* type, size_t width, size_t height, size_t buffers,
@@ -67,6 +76,9 @@ YRT_API YRTHandle yrtNewFrameBuffer(YRTDevice dev, const char* type, size_t widt
 YRT_API int yrtIncRef(YRTDevice dev, YRTHandle h);
 YRT_API int yrtDecRef(YRTDevice dev, YRTHandle h);
 YRT_API int yrtSetBool1(YRTDevice dev, YRTHandle h, const char* property, int x);
+YRT_API int yrtSetBool2(YRTDevice dev, YRTHandle h, const char* property, int x, int y);
+YRT_API int yrtSetBool3(YRTDevice dev, YRTHandle h, const char* property, int x, int y, int z);
+YRT_API int yrtSetBool4(YRTDevice dev, YRTHandle h, const char* property, int x, int y, int z, int w);
 YRT_API int yrtSetInt1(YRTDevice dev, YRTHandle h, const char* property, int x);
 YRT_API int yrtSetInt2(YRTDevice dev, YRTHandle h, const char* property, int x, int y);
 YRT_API int yrtSetInt3(YRTDevice dev, YRTHandle h, const char* property, int x, int y, int z);
@@ -75,7 +87,12 @@ YRT_API int yrtSetFloat1(YRTDevice dev, YRTHandle h, const char* property, float
 YRT_API int yrtSetFloat2(YRTDevice dev, YRTHandle h, const char* property, float x, float y);
 YRT_API int yrtSetFloat3(YRTDevice dev, YRTHandle h, const char* property, float x, float y, float z);
 YRT_API int yrtSetFloat4(YRTDevice dev, YRTHandle h, const char* property, float x, float y, float z, float w);
+YRT_API int yrtGetFloat1(YRTDevice dev, YRTHandle h, const char* property, float* x);
 YRT_API int yrtGetFloat3(YRTDevice dev, YRTHandle h, const char* property, float* x, float* y, float* z);
+/* rtGetString (device.h:293): copies at most bufSize-1 bytes + NUL; returns the full length. */
+YRT_API int yrtGetString(YRTDevice dev, YRTHandle h, const char* property, char* buf, size_t bufSize);
+/* rtGetTransform (device.h:303): 12 floats (vx, vy, vz, p); identity when unset. */
+YRT_API int yrtGetTransform(YRTDevice dev, YRTHandle h, const char* property, float* transform12);
 YRT_API int yrtSetArray(YRTDevice dev, YRTHandle h, const char* property, const char* type, YRTHandle data,
                         size_t size, size_t stride, size_t ofs);
 YRT_API int yrtSetString(YRTDevice dev, YRTHandle h, const char* property, const char* str);
@@ -92,6 +109,10 @@ YRT_API int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, 
 YRT_API void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
 YRT_API int yrtUnmapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
 YRT_API int yrtSwapBuffers(YRTDevice dev, YRTHandle framebuffer);
+/* rtPick (device.h:329, singleray_device.cpp:692-708): world position of the closest hit of
+ * the camera ray through image-plane point (x, y) in [0,1]^2. Returns 1 hit, 0 miss, <0 error. */
+YRT_API int yrtPick(YRTDevice dev, YRTHandle camera, float x, float y, YRTHandle scene, float* px, float* py,
+                    float* pz);
 /* Renderer status callback (device.h:335-347): state 0 Inactive, 1 Rendering, 2 Done. */
 typedef void (*YRTStatusCallback)(int state, float progress, void* user);
 YRT_API int yrtSetStatusCallback(YRTDevice dev, YRTHandle renderer, YRTStatusCallback cb, void* user);

@@ -288,3 +288,91 @@ def test_params_rt_defaults():
 def test_start_rt_rejects_missing_and_collada(tmp_path):
     assert not yrt.StartRT(tmp_path / "x.txt")
     assert yrt.GetLastErrorRT() == 2  # MissingColladaFile
+
+
+# ----------------------------------------------------------------------------- remaining Device API
+def _quad_scene(d, face_camera):
+    mesh = d.rtNewShape("trianglemesh")
+    # authored lying in the XZ plane: the update's -90 degree turn about `right` stands it up
+    pos = np.array([[-1, 0, 0], [1, 0, 0], [1, 0, 2], [-1, 0, 2]], np.float32)
+    idx = np.array([[0, 1, 2], [2, 3, 0]], np.int32)
+    d.rtSetArray(mesh, "positions", "float3", d.rtNewData("immutable", pos), 4, 12)
+    d.rtSetArray(mesh, "indices", "int3", d.rtNewData("immutable", idx), 2, 12)
+    d.rtCommit(mesh)
+    mat = d.rtNewMaterial("Matte")
+    d.rtCommit(mat)
+    xf = np.array([2, 0, 0, 0, 2, 0, 0, 0, 2, 5, 0, 5], np.float32)  # scale 2, at (5, 0, 5)
+    prim = d.rtNewShapePrimitive(mesh, mat, xf, face_camera)
+    scene = d.rtNewScene("default")
+    d.rtSetPrimitive(scene, 0, prim)
+    d.rtCommit(scene)
+    return scene, prim
+
+
+def _tris(d, scene):
+    cam = d.rtNewCamera("pinhole")
+    d.rtCommit(cam)
+    r = d.rtNewRenderer("pathtracer")
+    d.rtCommit(r)
+    return oracle.scene_triangles(d.export_frame(r, cam, scene)).reshape(-1, 3, 3)
+
+
+def test_update_primitive_faces_camera(host_device):
+    """rtUpdatePrimitive (singleray_device.cpp:354-398): the faceCamera quad turns to face the
+    floor-projected camera direction, keeping its position and scale."""
+    d = host_device
+    scene, prim = _quad_scene(d, True)
+    cam_pos = (5.0, 3.0, 20.0)
+    d.rtUpdatePrimitive(scene, 0, prim, cam_pos, (0.0, 1.0, 0.0))
+    d.rtCommit(scene)
+    t = _tris(d, scene)
+    n = np.cross(t[0, 1] - t[0, 0], t[0, 2] - t[0, 0])
+    n /= np.linalg.norm(n)
+    to_eye = np.array([0.0, 0.0, 1.0])  # (cam - prim) projected on the floor
+    assert abs(abs(np.dot(n, to_eye)) - 1.0) < 1e-5
+    c = t.reshape(-1, 3).mean(0)
+    assert np.allclose(c[[0, 2]], [5.0, 5.0], atol=1e-4)
+    ext = t.reshape(-1, 3).max(0) - t.reshape(-1, 3).min(0)
+    assert np.isclose(max(ext), 4.0, atol=1e-4)  # 2 (mesh) x 2 (scale)
+
+
+def test_update_primitive_ignores_static(host_device):
+    d = host_device
+    scene, prim = _quad_scene(d, False)
+    before = _tris(d, scene)
+    d.rtUpdatePrimitive(scene, 0, prim, (0.0, 0.0, 50.0), (0.0, 1.0, 0.0))
+    d.rtCommit(scene)
+    assert np.array_equal(before, _tris(d, scene))
+
+
+def test_transform_primitive_composes(host_device):
+    """rtTransformPrimitive: new transform = given * primitive's (api/instance.h:47-51)."""
+    d = host_device
+    scene, prim = _quad_scene(d, False)
+    moved = d.rtTransformPrimitive(prim, np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 10, 0], np.float32))
+    s2 = d.rtNewScene("default")
+    d.rtSetPrimitive(s2, 0, moved)
+    d.rtCommit(s2)
+    a, b = _tris(d, scene), _tris(d, s2)
+    assert np.allclose(b - a, np.array([0, 10, 0], np.float32))
+
+
+def test_getters_and_data_from_file(host_device, tmp_path):
+    d = host_device
+    cam = d.rtNewCamera("pinhole")
+    d.rtSetFloat1(cam, "sceneScale", 2.5)
+    d.rtSetString(cam, "name", "cam_front")
+    xf = np.arange(12, dtype=np.float32)
+    d.rtSetTransform(cam, "local2world", xf)
+    assert d.rtGetFloat1(cam, "sceneScale") == 2.5
+    assert d.rtGetFloat1(cam, "unset") == 0.0
+    assert d.rtGetString(cam, "name") == "cam_front"
+    assert np.array_equal(d.rtGetTransform(cam, "local2world"), xf)
+    assert np.array_equal(d.rtGetTransform(cam, "nothing"), [1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0])
+    d.rtSetBool2(cam, "b2", 1, 0)
+    d.rtSetBool4(cam, "b4", 1, 0, 1, 0)
+    f = tmp_path / "blob.bin"
+    f.write_bytes(bytes(range(64)))
+    assert d.rtNewDataFromFile("immutable", f, 8, 16)
+    with pytest.raises(RuntimeError):
+        d.rtNewDataFromFile("immutable", f, 60, 16)

@@ -162,3 +162,23 @@ def test_progressive_accumulate(gpu_device):
     assert np.isfinite(b).all() and not np.array_equal(a, b)
     assert abs(float(b.mean()) - float(a.mean())) < 0.25 * float(a.mean()) + 1e-3
     s.close()
+
+
+def test_pick(gpu_device):
+    """rtPick (singleray_device.cpp:692-708): centre of the Cornell view hits the back wall
+    (z = 559.2 in models/cornell_box.obj), matching the oracle's closest hit on that ray."""
+    s = _session(gpu_device, c1_args(64, 1))
+    i = s.info()
+    cam = s.camera()
+    hit, p = gpu_device.rtPick(cam, 0.5, 0.5, i["scene"])
+    assert hit
+    blob = s.export_frame()
+    # the pinhole ray through (0.5, 0.5): origin (278, 273, -800), towards +z
+    org = np.array([[278.0, 273.0, -800.0, 0.0]], np.float32)
+    d = np.array(p, np.float64) - org[0, :3]
+    dir4 = np.array([[*(d / np.linalg.norm(d)), np.inf]], np.float32)
+    ref = oracle.trace(blob, org, dir4)
+    q = org[0, :3] + ref[0, 0] * dir4[0, :3]
+    np.testing.assert_allclose(p, q, rtol=1e-4, atol=1e-2)
+    assert abs(p[2] - 559.2) < 1.0
+    s.close()

@@ -120,6 +120,7 @@ YRT_HD V3 xfmPoint(A3 m, V3 p) { return mul(m.l, p) + m.p; }
 YRT_HD V3 xfmVector(A3 m, V3 v) { return mul(m.l, v); }
 YRT_HD V3 xfmNormal(A3 m, V3 n) { return mul(transposed(inverse(m.l)), n); }
 YRT_HD A3 a3_translate(V3 p) { return a3(l3_identity(), p); }
+YRT_HD A3 a3_scale(V3 s) { return a3(l3(v3(s.x, 0, 0), v3(0, s.y, 0), v3(0, 0, s.z)), v3s(0.0f)); }
 YRT_HD A3 a3_rotate(V3 u, float r) { return a3(l3_rotate(u, r), v3s(0.0f)); }
 YRT_HD A3 a3_rotate_about(V3 p, V3 u, float r) {
   return mul(mul(a3_translate(p), a3_rotate(u, r)), a3_translate(-p));

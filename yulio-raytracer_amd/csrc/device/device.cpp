@@ -436,6 +436,24 @@ YRTHandle yrtNewData(YRTDevice dev, const char* type, size_t bytes, const void* 
   DEV_END(nullptr)
 }
 
+// SingleRayDevice::rtNewDataFromFile (singleray_device.cpp:204-222)
+YRTHandle yrtNewDataFromFile(YRTDevice dev, const char* type, const char* file, size_t offset, size_t bytes) {
+  DEV_GUARD(dev, nullptr)
+  if (!file) throw std::runtime_error("invalid file name");
+  if (!strncmp(file, "server:", 7)) file += 7;
+  if (strcasecmp(type, "immutable") != 0) throw std::runtime_error(std::string("unknown data buffer type: ") + type);
+  FILE* f = fopen(file, "rb");
+  if (!f) throw std::runtime_error(std::string("cannot open file ") + file);
+  auto d = std::make_shared<DataObj>();
+  d->bytes.resize(bytes);
+  fseek(f, (long)offset, SEEK_SET);
+  const size_t got = fread(d->bytes.data(), 1, bytes, f);
+  fclose(f);
+  if (got != bytes) throw std::runtime_error("error filling data buffer from file");
+  return dev->d->wrap(d);
+  DEV_END(nullptr)
+}
+
 YRTHandle yrtNewImage(YRTDevice dev, const char* type, size_t width, size_t height, const void* data) {
   DEV_GUARD(dev, nullptr)
   auto o = std::make_shared<ImageObj>();
@@ -523,6 +541,18 @@ YRTHandle yrtNewLightPrimitive(YRTDevice dev, YRTHandle light, YRTHandle materia
   DEV_END(nullptr)
 }
 
+// SingleRayDevice::rtTransformPrimitive (singleray_device.cpp:328-334) ->
+// PrimitiveHandle(space, other): transform = space * other.transform (api/instance.h:47-51)
+YRTHandle yrtTransformPrimitive(YRTDevice dev, YRTHandle prim, const float* transform12) {
+  DEV_GUARD(dev, nullptr)
+  auto o = dev->d->get<PrimitiveObj>(prim, "primitive");
+  if (!o) throw std::runtime_error("invalid primitive handle");
+  auto p = std::make_shared<PrimitiveObj>(*o);
+  p->transform = mul(xfm_or_identity(transform12), o->transform);
+  return dev->d->wrap(p);
+  DEV_END(nullptr)
+}
+
 YRTHandle yrtNewScene(YRTDevice dev, const char* type) {
   DEV_GUARD(dev, nullptr)
   return dev->d->wrap(std::make_shared<SceneObj>(type ? type : "default"));
@@ -558,6 +588,63 @@ int yrtSetPrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim)
   sp->shadowMask = p->shadowMask;
   sp->faceCamera = p->faceCamera;
   sp->prim = p;
+  s->slots[slot] = sp;
+  return 0;
+  DEV_END(-1)
+}
+
+// SingleRayDevice::rtUpdatePrimitive (singleray_device.cpp:354-398): re-orients a faceCamera
+// primitive toward the camera position projected on the floor and replaces the scene slot
+// (BackendSceneFlat::Handle::updatePrimitive, api/scene_flat.h:75-85). The caller re-commits
+// the scene (renderer.cpp:550-559).
+int yrtUpdatePrimitive(YRTDevice dev, YRTHandle scene, size_t slot, YRTHandle prim, const float* camPos3,
+                       const float* camUp3) {
+  DEV_GUARD(dev, -1)
+  auto s = dev->d->get<SceneObj>(scene, "scene");
+  if (!s) throw std::runtime_error("invalid scene handle");
+  if (!prim) {
+    if (slot < s->slots.size()) s->slots[slot].reset();
+    return 0;
+  }
+  auto p = dev->d->get<PrimitiveObj>(prim, "primitive");
+  if (!p->faceCamera) return 0;
+  const V3 camPos = v3(camPos3[0], camPos3[1], camPos3[2]);
+  const V3 camUp = v3(camUp3[0], camUp3[1], camUp3[2]);
+  const V3 primPos = p->transform.p;
+  V3 toEye = camPos - primPos;
+  toEye.y = 0.f;
+  toEye = normalize(toEye);
+  const A3 lookAt = lookAtPoint(v3s(0.f), toEye, camUp);
+  V3 right = cross(camUp, v3(0.f, 0.f, 1.f));
+  if (right.x == 0.f && right.y == 0.f && right.z == 0.f) right = cross(camUp, v3(0.f, 1.f, 0.f));
+  if (right.x == 0.f && right.y == 0.f && right.z == 0.f) right = cross(camUp, v3(1.f, 0.f, 0.f));
+  const A3 makeVertical = a3_rotate_about(v3s(0.f), right, deg2rad(-90.f));
+  A3 xf = mul(mul(a3_translate(primPos), lookAt), makeVertical);
+  // glm::decompose scale: column lengths, negated when the linear part flips orientation
+  const L3& l = p->transform.l;
+  V3 sc = v3(length(l.vx), length(l.vy), length(l.vz));
+  if (dot(l.vx, cross(l.vy, l.vz)) < 0.f) sc = -sc;
+  if (sc.x != 0.f && sc.y != 0.f && sc.z != 0.f) xf = mul(xf, a3_scale(sc));
+  if (slot > s->slots.size()) return 0;
+  if (slot == s->slots.size()) s->slots.resize(slot + 1);
+  auto sp = std::make_shared<ScenePrim>();
+  std::shared_ptr<const MeshInst> shape;
+  std::shared_ptr<const LightInst> light;
+  if (p->shapeHandle && p->shapeHandle->inst) shape = p->shapeHandle->inst;
+  if (p->lightHandle && p->lightHandle->inst) {
+    light = p->lightHandle->inst;
+    shape = light->shape;
+  }
+  if (shape) sp->shape = shape->transform(xf);
+  if (light) sp->light = light->transform(xf, p->illumMask, p->shadowMask);
+  if (p->materialHandle) sp->material = p->materialHandle->inst;
+  sp->illumMask = p->illumMask;
+  sp->shadowMask = p->shadowMask;
+  sp->faceCamera = true;
+  auto exportPrim = std::make_shared<PrimitiveObj>(*p);
+  exportPrim->transform = xf;  // the frame blob carries the applied transform
+  exportPrim->faceCamera = false;
+  sp->prim = exportPrim;
   s->slots[slot] = sp;
   return 0;
   DEV_END(-1)
@@ -617,13 +704,32 @@ int yrtDecRef(YRTDevice dev, YRTHandle h) {
 static int set_variant(YRTDevice dev, YRTHandle h, const char* prop, const Variant& v) {
   DEV_GUARD(dev, -1)
   if (!prop) throw std::runtime_error("invalid property");
-  dev->d->ref(h)->obj->parms.set(prop, v);
+  auto& obj = dev->d->ref(h)->obj;
+  obj->parms.set(prop, v);
+  // PrimitiveHandle::set applies immediately (api/instance.h:54-60)
+  if (auto p = std::dynamic_pointer_cast<PrimitiveObj>(obj)) {
+    if (!strcmp(prop, "illumMask")) p->illumMask = v.i[0];
+    else if (!strcmp(prop, "shadowMask")) p->shadowMask = v.i[0];
+    else if (!strcmp(prop, "faceCamera")) p->faceCamera = v.i[0] != 0;
+  }
   return 0;
   DEV_END(-1)
 }
 
 int yrtSetBool1(YRTDevice dev, YRTHandle h, const char* p, int x) {
   Variant v; v.type = Variant::BOOL1; v.i[0] = x != 0;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetBool2(YRTDevice dev, YRTHandle h, const char* p, int x, int y) {
+  Variant v; v.type = Variant::BOOL2; v.i[0] = x != 0; v.i[1] = y != 0;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetBool3(YRTDevice dev, YRTHandle h, const char* p, int x, int y, int z) {
+  Variant v; v.type = Variant::BOOL3; v.i[0] = x != 0; v.i[1] = y != 0; v.i[2] = z != 0;
+  return set_variant(dev, h, p, v);
+}
+int yrtSetBool4(YRTDevice dev, YRTHandle h, const char* p, int x, int y, int z, int w) {
+  Variant v; v.type = Variant::BOOL4; v.i[0] = x != 0; v.i[1] = y != 0; v.i[2] = z != 0; v.i[3] = w != 0;
   return set_variant(dev, h, p, v);
 }
 int yrtSetInt1(YRTDevice dev, YRTHandle h, const char* p, int x) {
@@ -663,6 +769,42 @@ int yrtGetFloat3(YRTDevice dev, YRTHandle h, const char* p, float* x, float* y, 
   const Variant* v = dev->d->ref(h)->obj->parms.find(p);
   if (!v || v->type != Variant::FLOAT3) throw std::runtime_error(std::string("no float3 property ") + p);
   *x = v->f[0]; *y = v->f[1]; *z = v->f[2];
+  return 0;
+  DEV_END(-1)
+}
+// rtGetFloat1 / rtGetString / rtGetTransform (singleray_device.cpp:548-555, 616-622, 651-657):
+// the reference reads the handle's current value; unset properties read as 0 / "" / identity.
+int yrtGetFloat1(YRTDevice dev, YRTHandle h, const char* p, float* x) {
+  DEV_GUARD(dev, -1)
+  if (!h) return 0;
+  const Variant* v = dev->d->ref(h)->obj->parms.find(p);
+  *x = 0.f;
+  if (v) {
+    if (v->type >= Variant::FLOAT1 && v->type <= Variant::FLOAT4) *x = v->f[0];
+    else if (v->type >= Variant::BOOL1 && v->type <= Variant::INT4) *x = (float)v->i[0];
+  }
+  return 0;
+  DEV_END(-1)
+}
+int yrtGetString(YRTDevice dev, YRTHandle h, const char* p, char* buf, size_t bufSize) {
+  DEV_GUARD(dev, -1)
+  if (!h) return 0;
+  const Variant* v = dev->d->ref(h)->obj->parms.find(p);
+  const std::string str = (v && v->type == Variant::STRING) ? v->str : std::string();
+  if (buf && bufSize) {
+    const size_t n = std::min(bufSize - 1, str.size());
+    memcpy(buf, str.data(), n);
+    buf[n] = 0;
+  }
+  return (int)str.size();
+  DEV_END(-1)
+}
+int yrtGetTransform(YRTDevice dev, YRTHandle h, const char* p, float* transform12) {
+  DEV_GUARD(dev, -1)
+  if (!h) return 0;
+  const Variant* v = dev->d->ref(h)->obj->parms.find(p);
+  static const float I[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+  memcpy(transform12, (v && v->type == Variant::TRANSFORM) ? v->f : I, sizeof(I));
   return 0;
   DEV_END(-1)
 }
@@ -814,6 +956,28 @@ int yrtTriangleIds(YRTDevice dev, YRTHandle scene, int32_t tri, int32_t* geomID,
   return 0;
   DEV_END(-1)
 }
+int yrtPick(YRTDevice dev, YRTHandle camera, float x, float y, YRTHandle scene, float* px, float* py, float* pz) {
+  DEV_GUARD(dev, -1)
+  Device& D = *dev->d;
+  if (!D.gpu) throw std::runtime_error("rtPick: host-only device");
+  auto C = D.get<CameraObj>(camera, "camera");
+  auto S = D.get<SceneObj>(scene, "scene");
+  if (!C || !S || !S->gpu) throw std::runtime_error("rtPick: invalid camera or uncommitted scene");
+  HIP_CHECK(hipSetDevice(D.hipDevice));
+  D.dCam.alloc(sizeof(GpuCamera));
+  D.dCount.alloc(sizeof(float4));
+  HIP_CHECK(hipMemcpyAsync(D.dCam.p, &C->cam, sizeof(GpuCamera), hipMemcpyHostToDevice, D.stream));
+  launch_pick(S->gpu->view, D.dCam.as<GpuCamera>(), x, y, D.dCount.as<float4>(), D.stream);
+  float4 r;
+  HIP_CHECK(hipMemcpyAsync(&r, D.dCount.p, sizeof(r), hipMemcpyDeviceToHost, D.stream));
+  HIP_CHECK(hipStreamSynchronize(D.stream));
+  *px = r.x;
+  *py = r.y;
+  *pz = r.z;
+  return __builtin_bit_cast(int, r.w) >= 0 ? 1 : 0;
+  DEV_END(-1)
+}
+
 int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out) {
   DEV_GUARD(dev, -1)
   *out = dev->d->stats;

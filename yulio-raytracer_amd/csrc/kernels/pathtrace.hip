@@ -838,6 +838,29 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
                      fbFloat, fbRGB8, rgb8Stride, accu, accumulate);
 }
 
+// SingleRayDevice::rtPick (api/singleray_device.cpp:692-708): one camera ray at image-plane
+// (x, y), lens sample (0.5, 0.5), closest hit.
+__global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_pick(SceneView sv, const GpuCamera* camp, float x, float y,
+                                                          float4* out) {
+  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  if (threadIdx.x != 0) return;
+  V3 org, dir;
+  camera_ray(*camp, x, y, org, dir);
+  RayPre r;
+  r.org = org;
+  r.dir = dir;
+  r.inv = v3(safe_inv(dir.x), safe_inv(dir.y), safe_inv(dir.z));
+  r.tnear = 0.f;
+  r.tfar = __int_as_float(0x7f800000);
+  const Hit h = traverse<false>(sv.nodes, sv.tris, r, stack + threadIdx.x);
+  const V3 p = org + h.t * dir;
+  out[0] = make_float4(p.x, p.y, p.z, __int_as_float(h.tri));
+}
+
+void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(YRT_TRACE_BLOCK), 0, s, sv, cam, x, y, out);
+}
+
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s) {
   hipLaunchKernelGGL(k_debug, dim3((numTiles + 63) / 64), dim3(64), 0, s, sv, fv, maxDepth, spp, fbFloat, fbRGB8,

@@ -160,6 +160,51 @@ class Device:
         self._rc(N.dev.yrtGetFloat3(self.h, h, _b(p), C.byref(x), C.byref(y), C.byref(z)), "rtGetFloat3")
         return x.value, y.value, z.value
 
+    def rtSetBool2(self, h, p, x, y):
+        self._rc(N.dev.yrtSetBool2(self.h, h, _b(p), int(bool(x)), int(bool(y))), "rtSetBool2")
+
+    def rtSetBool3(self, h, p, x, y, z):
+        self._rc(N.dev.yrtSetBool3(self.h, h, _b(p), int(bool(x)), int(bool(y)), int(bool(z))), "rtSetBool3")
+
+    def rtSetBool4(self, h, p, x, y, z, w):
+        self._rc(N.dev.yrtSetBool4(self.h, h, _b(p), *[int(bool(v)) for v in (x, y, z, w)]), "rtSetBool4")
+
+    def rtGetFloat1(self, h, p):
+        x = C.c_float()
+        self._rc(N.dev.yrtGetFloat1(self.h, h, _b(p), C.byref(x)), "rtGetFloat1")
+        return x.value
+
+    def rtGetString(self, h, p):
+        n = N.dev.yrtGetString(self.h, h, _b(p), None, 0)
+        if n < 0:
+            raise RuntimeError(f"rtGetString: {self.error()}")
+        buf = C.create_string_buffer(n + 1)
+        N.dev.yrtGetString(self.h, h, _b(p), buf, n + 1)
+        return buf.value.decode()
+
+    def rtGetTransform(self, h, p):
+        out = (C.c_float * 12)()
+        self._rc(N.dev.yrtGetTransform(self.h, h, _b(p), out), "rtGetTransform")
+        return np.array(out, np.float32)
+
+    def rtNewDataFromFile(self, type, file, offset, bytes_):
+        return self._h(N.dev.yrtNewDataFromFile(self.h, _b(type), _b(str(file)), offset, bytes_), "rtNewDataFromFile")
+
+    def rtTransformPrimitive(self, prim, transform):
+        return self._h(N.dev.yrtTransformPrimitive(self.h, prim, _xfm(transform)), "rtTransformPrimitive")
+
+    def rtUpdatePrimitive(self, scene, slot, prim, camPos, camUp):
+        pos = (C.c_float * 3)(*camPos)
+        up = (C.c_float * 3)(*camUp)
+        self._rc(N.dev.yrtUpdatePrimitive(self.h, scene, slot, prim, pos, up), "rtUpdatePrimitive")
+
+    def rtPick(self, camera, x, y, scene):
+        px, py, pz = C.c_float(), C.c_float(), C.c_float()
+        r = N.dev.yrtPick(self.h, camera, float(x), float(y), scene, C.byref(px), C.byref(py), C.byref(pz))
+        if r < 0:
+            raise RuntimeError(f"rtPick: {self.error()}")
+        return bool(r), (px.value, py.value, pz.value)
+
     def rtSetArray(self, h, p, type, data, size, stride, ofs=0):
         self._rc(N.dev.yrtSetArray(self.h, h, _b(p), _b(type), data, size, stride, ofs), "rtSetArray")
 

@@ -96,6 +96,9 @@ _sig(dev, "yrtNewFrameBuffer", vp, vp, cstr, sz, sz, sz, vp)
 _sig(dev, "yrtIncRef", i32, vp, vp)
 _sig(dev, "yrtDecRef", i32, vp, vp)
 _sig(dev, "yrtSetBool1", i32, vp, vp, cstr, i32)
+_sig(dev, "yrtSetBool2", i32, vp, vp, cstr, i32, i32)
+_sig(dev, "yrtSetBool3", i32, vp, vp, cstr, i32, i32, i32)
+_sig(dev, "yrtSetBool4", i32, vp, vp, cstr, i32, i32, i32, i32)
 _sig(dev, "yrtSetInt1", i32, vp, vp, cstr, i32)
 _sig(dev, "yrtSetInt2", i32, vp, vp, cstr, i32, i32)
 _sig(dev, "yrtSetInt3", i32, vp, vp, cstr, i32, i32, i32)
@@ -104,7 +107,14 @@ _sig(dev, "yrtSetFloat1", i32, vp, vp, cstr, f32)
 _sig(dev, "yrtSetFloat2", i32, vp, vp, cstr, f32, f32)
 _sig(dev, "yrtSetFloat3", i32, vp, vp, cstr, f32, f32, f32)
 _sig(dev, "yrtSetFloat4", i32, vp, vp, cstr, f32, f32, f32, f32)
+_sig(dev, "yrtGetFloat1", i32, vp, vp, cstr, PF)
 _sig(dev, "yrtGetFloat3", i32, vp, vp, cstr, PF, PF, PF)
+_sig(dev, "yrtGetString", i32, vp, vp, cstr, C.c_char_p, sz)
+_sig(dev, "yrtGetTransform", i32, vp, vp, cstr, PF)
+_sig(dev, "yrtNewDataFromFile", vp, vp, cstr, cstr, sz, sz)
+_sig(dev, "yrtTransformPrimitive", vp, vp, vp, PF)
+_sig(dev, "yrtUpdatePrimitive", i32, vp, vp, sz, vp, PF, PF)
+_sig(dev, "yrtPick", i32, vp, vp, f32, f32, vp, PF, PF, PF)
 _sig(dev, "yrtSetArray", i32, vp, vp, cstr, cstr, vp, sz, sz, sz)
 _sig(dev, "yrtSetString", i32, vp, vp, cstr, cstr)
 _sig(dev, "yrtSetImage", i32, vp, vp, cstr, vp)
