@@ -50,20 +50,31 @@ class Device {
   int captureMax = 0;
   struct Captured { std::vector<float> org, dir; double total = 0; };
   std::vector<Captured> capClosest, capShadow;
-  void capture(std::vector<Captured>& out, int depth, const float4* org, const float4* dir, const unsigned* dcount) {
-    unsigned n = 0;
-    HIP_CHECK(hipMemcpyAsync(&n, dcount, sizeof(n), hipMemcpyDeviceToHost, stream));
+  // counts: the queue's first segment counter; segments of segCap slots
+  void capture(std::vector<Captured>& out, int depth, const float4* org, const float4* dir, const unsigned* counts,
+               int segCap) {
+    std::vector<unsigned> cs((size_t)YRT_QSEGS * YRT_QCSTRIDE);
+    HIP_CHECK(hipMemcpyAsync(cs.data(), counts, cs.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
+    size_t n = 0;
+    for (int k = 0; k < YRT_QSEGS; ++k) n += cs[(size_t)k * YRT_QCSTRIDE];
     if ((int)out.size() <= depth) out.resize(depth + 1);
     Captured& c = out[depth];
-    c.total = n;
+    c.total = (double)n;
+    c.org.clear();
+    c.dir.clear();
     const size_t stride = std::max<size_t>(1, (n + captureMax - 1) / captureMax);
-    const size_t m = n ? (n + stride - 1) / stride : 0;
-    c.org.resize(m * 4);
-    c.dir.resize(m * 4);
-    if (m) {
-      HIP_CHECK(hipMemcpy2D(c.org.data(), 16, org, stride * 16, 16, m, hipMemcpyDeviceToHost));
-      HIP_CHECK(hipMemcpy2D(c.dir.data(), 16, dir, stride * 16, 16, m, hipMemcpyDeviceToHost));
+    for (int k = 0; k < YRT_QSEGS; ++k) {
+      const size_t nk = cs[(size_t)k * YRT_QCSTRIDE];
+      const size_t m = nk ? (nk + stride - 1) / stride : 0;
+      if (!m) continue;
+      const size_t at = c.org.size();
+      c.org.resize(at + m * 4);
+      c.dir.resize(at + m * 4);
+      HIP_CHECK(hipMemcpy2D(c.org.data() + at, 16, org + (size_t)k * segCap, stride * 16, 16, m,
+                            hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy2D(c.dir.data() + at, 16, dir + (size_t)k * segCap, stride * 16, 16, m,
+                            hipMemcpyDeviceToHost));
     }
   }
 
@@ -106,20 +117,22 @@ class Device {
     return o;
   }
 
+  // P paths per batch; queues hold YRT_QSEGS segments of qseg_capacity(P) slots
   void ensure_paths(int64_t P, int numLights) {
-    if (P > pathCap) {
+    const int64_t Q = (int64_t)YRT_QSEGS * qseg_capacity(P);
+    if (Q > pathCap) {
       for (int k = 0; k < 2; ++k) {
-        qPath[k].alloc(P * 4);
-        qOrg[k].alloc(P * 16);
-        qDir[k].alloc(P * 16);
+        qPath[k].alloc(Q * 4);
+        qOrg[k].alloc(Q * 16);
+        qDir[k].alloc(Q * 16);
       }
-      hit.alloc(P * 16);
-      thr.alloc(P * 16);
-      L.alloc(P * 16);
-      meta.alloc(P * 4);
-      pathCap = P;
+      hit.alloc(Q * 16);
+      thr.alloc(Q * 16);
+      L.alloc(Q * 16);
+      meta.alloc(Q * 4);
+      pathCap = Q;
     }
-    const int64_t S = P * std::max(1, numLights);
+    const int64_t S = Q * std::max(1, numLights);
     if (S > shadowCap) {
       shFirst.alloc(S * 4);
       sOrg.alloc(S * 16);
@@ -247,9 +260,10 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
     ensure_paths(std::max<int64_t>(P, 256ll * spp), rp.numLights);
     const int levels = rp.maxDepth + 1;
-    dCounters.alloc((size_t)levels * 4 * sizeof(unsigned));
+    const size_t counterWords = qcounter_index(levels, 0, 0);
+    dCounters.alloc(counterWords * sizeof(unsigned));
     dAccu.alloc((size_t)W * H * 16);
-    std::vector<unsigned> hc(levels * 4);
+    std::vector<unsigned> hc(counterWords);
     PathBuffers pb;
     for (int k = 0; k < 2; ++k) {
       pb.qPath[k] = qPath[k].as<int>();
@@ -267,7 +281,8 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     pb.sOcc = sOcc.as<int>();
     pb.counters = dCounters.as<unsigned>();
     pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
-    pb.shadowCapacity = (int)(pb.capacity * std::max(1, rp.numLights));
+    pb.segCap = qseg_capacity(pb.capacity);
+    pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
 
     struct EvPair { hipEvent_t a, b; int kind; };
     std::vector<EvPair> evs;
@@ -278,15 +293,17 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
       bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
       bi.tileStride = shardCount;
       bi.tileOffset = shardIndex;
-      HIP_CHECK(hipMemsetAsync(dCounters.p, 0, (size_t)levels * 4 * sizeof(unsigned), stream));
+      HIP_CHECK(hipMemsetAsync(dCounters.p, 0, counterWords * sizeof(unsigned), stream));
       launch_raygen(fv, pb, bi, stream);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
         EvPair e1{};
         if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, stream)); }
-        launch_trace_closest(G.view, pb.qOrg[cur], pb.qDir[cur], pb.counters + d * 4, pb.capacity, pb.hit, stream);
+        launch_trace_closest(G.view, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
+                             pb.segCap, pb.hit, stream);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, stream)); evs.push_back(e1); }
-        if (captureMax > 0 && first == 0) capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + d * 4);
+        if (captureMax > 0 && first == 0)
+          capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap);
         EvPair e2{};
         if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
         launch_shade(G.view, fv, pb, bi, d, stream);
@@ -294,9 +311,11 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         if (rp.numLights > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
-          launch_trace_any(G.view, pb.sOrg, pb.sDir, pb.counters + d * 4 + 1, pb.shadowCapacity, pb.sOcc, stream);
+          launch_trace_any(G.view, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
+                           pb.sOcc, stream);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
-          if (captureMax > 0 && first == 0) capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + d * 4 + 1);
+          if (captureMax > 0 && first == 0)
+            capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap);
           launch_shadow_resolve(pb, d, rp.numLights, stream);
         }
       }
@@ -305,10 +324,17 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
       HIP_CHECK(hipMemcpyAsync(hc.data(), dCounters.p, hc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
       HIP_CHECK(hipStreamSynchronize(stream));
       for (int d = 0; d < levels; ++d) {
-        stats.raysClosest += hc[d * 4 + 0];
-        stats.raysShadow += hc[d * 4 + 1];
-        if (d < rp.maxDepth && hc[d * 4 + 0]) stats.launchesClosest += 1;
-        if (d < rp.maxDepth && hc[d * 4 + 1]) stats.launchesShadow += 1;
+        double nc = 0, ns = 0;
+        for (int k = 0; k < YRT_QSEGS; ++k) {
+          nc += hc[qcounter_index(d, 0, k)];
+          ns += hc[qcounter_index(d, 1, k)];
+        }
+        if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
+          stats.raysClosest += nc;
+          if (nc) stats.launchesClosest += 1;
+        }
+        stats.raysShadow += ns;
+        if (d < rp.maxDepth && ns) stats.launchesShadow += 1;
       }
       status(R, 1, float(first + bi.numPixels / 256) / float(std::max(1, shardTiles)));
     }
@@ -360,9 +386,9 @@ void Device::intersect(SceneObj& S, const float* org4, const float* dir4, uint32
   dCount.alloc(sizeof(unsigned));
   HIP_CHECK(hipMemcpyAsync(dCount.p, &n, sizeof(unsigned), hipMemcpyHostToDevice, st));
   if (occ)
-    launch_trace_any(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), (int)n, occ, st);
+    launch_trace_any(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n, occ, st);
   else
-    launch_trace_closest(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), (int)n,
+    launch_trace_closest(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n,
                          (float4*)hit4, st);
   HIP_CHECK(hipStreamSynchronize(st));
 }

@@ -55,6 +55,40 @@ __device__ __forceinline__ unsigned wave_append(unsigned* counter, bool pred, bo
   return base + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
+// ---------------------------------------------------------------- segmented queues
+struct QMap {
+  unsigned pre[YRT_QSEGS + 1];  // exclusive prefix of the segment counts; pre[numSegs] = total
+};
+
+// Every thread of the block must call it (barrier inside).
+__device__ __forceinline__ void qmap_load(QMap& m, const unsigned* counts, int numSegs) {
+  if (threadIdx.x == 0) {
+    unsigned c[YRT_QSEGS];
+#pragma unroll
+    for (int k = 0; k < YRT_QSEGS; ++k) c[k] = k < numSegs ? counts[(size_t)k * YRT_QCSTRIDE] : 0u;
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < YRT_QSEGS; ++k) {
+      m.pre[k] = acc;
+      acc += c[k];
+    }
+    m.pre[YRT_QSEGS] = acc;
+  }
+  __syncthreads();
+}
+
+// Physical slot of logical queue index q < total.
+__device__ __forceinline__ int qmap_phys(const QMap& m, int segCap, unsigned q) {
+  int lo = 0;
+#pragma unroll
+  for (int step = YRT_QSEGS / 2; step > 0; step >>= 1)
+    if (m.pre[lo + step] <= q) lo += step;
+  return lo * segCap + (int)(q - m.pre[lo]);
+}
+
+// Segment that input item q appends into (uniform across a wave: q >> 6 is).
+__device__ __forceinline__ int qseg_of(unsigned q) { return (int)((q >> 6) % YRT_QSEGS); }
+
 // ---------------------------------------------------------------- reference RNG
 // Park-Miller minimal standard + Bays-Durham shuffle (common/math/random.h:24-78).
 struct DevRandom {
@@ -217,7 +251,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
     }
     bool got;
-    const unsigned q = wave_append(&pb.counters[0], valid, got);
+    const int seg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
+    const unsigned q = seg * pb.segCap + wave_append(pb.counters + qcounter_index(0, 0, seg), valid, got);
     if (got) {
       pb.qPath[0][q] = p;
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
@@ -229,13 +264,16 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 template <bool ANY>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
-                                                         const unsigned* __restrict__ countp,
-                                                         float4* __restrict__ hitOut, int* __restrict__ occOut) {
+                                                         const unsigned* __restrict__ counts, int numSegs,
+                                                         int segCap, float4* __restrict__ hitOut,
+                                                         int* __restrict__ occOut) {
   __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
-  const int n = (int)*countp;
+  __shared__ QMap qm;
+  qmap_load(qm, counts, numSegs);
+  const int n = (int)qm.pre[YRT_QSEGS];
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const int q = base + threadIdx.x;
-    if (q >= n) break;
+    if (base + (int)threadIdx.x >= n) break;
+    const int q = qmap_phys(qm, segCap, (unsigned)(base + threadIdx.x));
     const float4 o = org[q], d = dir[q];
     RayPre r;
     r.org = v3(o.x, o.y, o.z);
@@ -496,14 +534,18 @@ __device__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy,
 __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
   const GpuRenderParams& rp = *fv.rp;
-  const int n = (int)pb.counters[depthLevel * 4 + 0];
+  __shared__ QMap qm;
+  qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
+  const int n = (int)qm.pre[YRT_QSEGS];
   const int cur = depthLevel & 1;
   const int numLights = sv.numLights;
-  unsigned* nextCount = &pb.counters[(depthLevel + 1) * 4 + 0];
-  unsigned* shadowCount = &pb.counters[depthLevel * 4 + 1];
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const int q = base + threadIdx.x;
-    const bool active = q < n;
+    const unsigned ql = (unsigned)base + threadIdx.x;
+    const bool active = (int)ql < n;
+    const int q = active ? qmap_phys(qm, pb.segCap, ql) : 0;
+    const int oseg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
+    unsigned* nextCount = pb.counters + qcounter_index(depthLevel + 1, 0, oseg);
+    unsigned* shadowCount = pb.counters + qcounter_index(depthLevel, 1, oseg);
     int path = 0;
     V3 org = v3s(0.f), dir = v3s(0.f), thr = v3s(0.f), L = v3s(0.f);
     int meta = 0, depth = 0, rec = 0, pixelId = 0, s = 0;
@@ -600,7 +642,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
         }
       }
       bool got;
-      const unsigned si = wave_append(shadowCount, pred, got);
+      const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, got);
       if (got) {
         pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
         pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
@@ -640,7 +682,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
       }
     }
     bool got;
-    const unsigned nq = wave_append(nextCount, cont, got);
+    const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
     if (got) {
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
@@ -651,9 +693,12 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
 
 // Adds the unoccluded direct-light terms in light order.
 __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, int depthLevel, int numLights) {
-  const int n = (int)pb.counters[depthLevel * 4 + 0];
+  __shared__ QMap qm;
+  qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
+  const int n = (int)qm.pre[YRT_QSEGS];
   const int cur = depthLevel & 1;
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+  for (int ql = blockIdx.x * blockDim.x + threadIdx.x; ql < n; ql += gridDim.x * blockDim.x) {
+    const int q = qmap_phys(qm, pb.segCap, (unsigned)ql);
     bool any = false;
     for (int li = 0; li < numLights; ++li) any |= pb.shFirst[(size_t)q * numLights + li] >= 0;
     if (!any) continue;
@@ -809,16 +854,18 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
   hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
 }
 
-void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count,
-                          int maxCount, float4* hit, hipStream_t s) {
+void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
+                          int numSegs, int segCap, float4* hit, hipStream_t s) {
+  const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
-                     sv, org, dir, count, hit, (int*)nullptr);
+                     sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr);
 }
 
-void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count, int maxCount,
-                      int* occluded, hipStream_t s) {
+void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
+                      int segCap, int* occluded, hipStream_t s) {
+  const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
-                     sv, org, dir, count, (float4*)nullptr, occluded);
+                     sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded);
 }
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,

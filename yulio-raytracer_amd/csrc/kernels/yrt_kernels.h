@@ -37,6 +37,23 @@ struct FrameView {
   int numRecords, numLightSlots;
 };
 
+// Queues are split into YRT_QSEGS segments, each with its own append counter on its own
+// 256-B line: one returning atomic on a single word saturates near 88 M/s on MI355X
+// (MI355X_MICROARCH.md, 'dequeue'), which bounded raygen/shade with one counter per queue.
+// Input item q appends into segment (q/64) % YRT_QSEGS, so a segment never receives more
+// than capacity/YRT_QSEGS + 64 items per input item's fan-out. Consumers map a logical index
+// to (segment, offset) through the exclusive prefix of the segment counts.
+#define YRT_QSEGS 32
+#define YRT_QCSTRIDE 64  // unsigned words between two segment counters
+// counters[((level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE], kind 0 = closest queue
+// entering depth `level`, kind 1 = shadow rays emitted at depth `level`.
+inline __host__ __device__ size_t qcounter_index(int level, int kind, int seg) {
+  return ((size_t)(level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE;
+}
+inline __host__ __device__ int qseg_capacity(long long items) {
+  return (int)(((items + 63) / 64 + YRT_QSEGS - 1) / YRT_QSEGS * 64 + 64);
+}
+
 // Wavefront state for one batch of P = numPixels * spp paths (SoA, device memory).
 struct PathBuffers {
   int* qPath[2];
@@ -51,9 +68,10 @@ struct PathBuffers {
   float4* sDir;
   float4* sContrib;
   int* sOcc;
-  unsigned* counters;  // [depth*4 + 0] queue size at depth, [depth*4+1] shadow rays at depth
+  unsigned* counters;  // segment counters, see qcounter_index
   int capacity;        // max paths
-  int shadowCapacity;  // max shadow rays per depth
+  int segCap;          // closest-queue slots per segment (qPath/qOrg/qDir/hit: YRT_QSEGS * segCap)
+  int shSegCap;        // shadow slots per segment (sOrg/sDir/sContrib/sOcc: YRT_QSEGS * shSegCap)
 };
 
 struct BatchInfo {
@@ -66,10 +84,12 @@ struct BatchInfo {
 // Kernel launchers (kernels/pathtrace.hip)
 void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int height, int sets, hipStream_t s);
 void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s);
-void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count,
-                          int maxCount, float4* hit, hipStream_t s);
-void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* count, int maxCount,
-                      int* occluded, hipStream_t s);
+// counts: first segment counter of the queue (segments YRT_QCSTRIDE apart), numSegs segments
+// of segCap slots; hit/occluded are indexed by physical slot.
+void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
+                          int numSegs, int segCap, float4* hit, hipStream_t s);
+void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
+                      int segCap, int* occluded, hipStream_t s);
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
                   hipStream_t s);
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
