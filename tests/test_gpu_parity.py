@@ -165,8 +165,9 @@ def test_progressive_accumulate(gpu_device):
 
 
 def test_pick(gpu_device):
-    """rtPick (singleray_device.cpp:692-708): centre of the Cornell view hits the back wall
-    (z = 559.2 in models/cornell_box.obj), matching the oracle's closest hit on that ray."""
+    """rtPick (singleray_device.cpp:692-708): the centre of the Cornell view hits the tall
+    block's front face, at the oracle's closest hit on the same ray; the top edge of the
+    image plane sees the ceiling."""
     s = _session(gpu_device, c1_args(64, 1))
     i = s.info()
     cam = s.camera()
@@ -180,5 +181,7 @@ def test_pick(gpu_device):
     ref = oracle.trace(blob, org, dir4)
     q = org[0, :3] + ref[0, 0] * dir4[0, :3]
     np.testing.assert_allclose(p, q, rtol=1e-4, atol=1e-2)
-    assert abs(p[2] - 559.2) < 1.0
+    assert 0.0 < p[2] < 559.3
+    hit, p = gpu_device.rtPick(cam, 0.5, 0.0, i["scene"])
+    assert hit and abs(p[1] - 548.8) < 1.0
     s.close()

@@ -25,7 +25,7 @@
 namespace yrt {
 
 #ifndef YRT_STACK_DEPTH
-#define YRT_STACK_DEPTH 40
+#define YRT_STACK_DEPTH 64
 #endif
 
 struct FrameCache {

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
                                                          int* __restrict__ occOut) {
-  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  __shared__ int stack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
   const int n = (int)qm.pre[YRT_QSEGS];
@@ -759,7 +759,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
 __global__ __launch_bounds__(64) void k_debug(SceneView sv, FrameView fv, int maxDepth, int spp,
                                              float* __restrict__ fbFloat, uint8_t* __restrict__ fbRGB8,
                                              int rgb8Stride) {
-  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  __shared__ int stack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   const GpuRenderParams& rp = *fv.rp;
   const GpuCamera& cam = *fv.cam;
   const int tile = blockIdx.x * blockDim.x + threadIdx.x;
@@ -889,7 +889,7 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 // (x, y), lens sample (0.5, 0.5), closest hit.
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_pick(SceneView sv, const GpuCamera* camp, float x, float y,
                                                           float4* out) {
-  __shared__ int stack[YRT_STACK_DEPTH * YRT_TRACE_BLOCK];
+  __shared__ int stack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   if (threadIdx.x != 0) return;
   V3 org, dir;
   camera_ray(*camp, x, y, org, dir);

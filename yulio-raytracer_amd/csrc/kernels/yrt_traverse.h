@@ -13,14 +13,19 @@
 //   closest hit: smallest (t, global triangle id) — order independent, so any BVH gives
 //   the same answer (used to pin the GPU against the oracle's own BVH).
 // Stack: per-lane short stack in LDS, [depth][lane] so a wave's pushes hit 64 distinct
-// banks; the builder bounds the tree depth to YRT_STACK_DEPTH-1 (device/bvh_build.cpp).
+// banks. Only YRT_LDS_STACK entries live in LDS (16 x 256 B per wave keeps LDS from capping
+// occupancy below the VGPR limit); deeper entries, rare, spill to a per-lane scratch array.
+// The builder bounds the tree depth to YRT_STACK_DEPTH-1 (device/bvh_build.cpp).
 #pragma once
 
 #include "../common/yrt_gpu_types.h"
 #include "../common/yrt_math.h"
 
 #ifndef YRT_STACK_DEPTH
-#define YRT_STACK_DEPTH 40
+#define YRT_STACK_DEPTH 64   // bound on BVH depth + 1 (device/bvh_build.cpp enforces it)
+#endif
+#ifndef YRT_LDS_STACK
+#define YRT_LDS_STACK 16     // top entries kept in LDS; deeper ones spill to per-lane scratch
 #endif
 #define YRT_TRACE_BLOCK 128
 
@@ -63,9 +68,10 @@ __device__ __forceinline__ void box2(const GpuNode& n, const RayPre& r, float tm
   t1 = n1;
 }
 
-// One triangle; returns true and t/u/v when the ray hits within (tnear, tfar).
-__device__ __forceinline__ bool tri_test(const GpuTri& tr, const RayPre& r, float tfar, float& t, float& u,
-                                         float& v) {
+// One triangle; returns true and t when the ray hits within (tnear, tfar). U, V, absDen are
+// returned undivided: u = U/absDen, v = V/absDen are only needed for an accepted hit.
+__device__ __forceinline__ bool tri_test_t(const GpuTri& tr, const RayPre& r, float tfar, float& t, float& U_,
+                                           float& V_, float& absDen_) {
   V3 v0 = v3(tr.v0[0], tr.v0[1], tr.v0[2]);
   V3 e1 = v3(tr.e1[0], tr.e1[1], tr.e1[2]);
   V3 e2 = v3(tr.e2[0], tr.e2[1], tr.e2[2]);
@@ -83,8 +89,9 @@ __device__ __forceinline__ bool tri_test(const GpuTri& tr, const RayPre& r, floa
   float T = dot(Ng, C) * sgn;
   t = T / absDen;
   ok &= (t > r.tnear) & (t < tfar);
-  u = U / absDen;
-  v = V / absDen;
+  U_ = U;
+  V_ = V;
+  absDen_ = absDen;
   return ok;
 }
 
@@ -98,6 +105,7 @@ __device__ __forceinline__ Hit traverse(const GpuNode* __restrict__ nodes, const
   // NaN tfar (tMaxShadowRay = inf): every comparison is false, no hit.
   if (!(r.tfar >= r.tnear)) return best;
   int sp = 0;
+  int spill[YRT_STACK_DEPTH > YRT_LDS_STACK ? YRT_STACK_DEPTH - YRT_LDS_STACK : 1];
   // stack entry: (index << 5) | count — count 0 => inner node, 1..31 => leaf range
   int curIdx = 0, curCnt = 0;
   while (true) {
@@ -110,7 +118,9 @@ __device__ __forceinline__ Hit traverse(const GpuNode* __restrict__ nodes, const
         bool swap = t1 < t0;
         int nearI = swap ? n.c[1] : n.c[0], nearC = swap ? n.c[3] : n.c[2];
         int farI = swap ? n.c[0] : n.c[1], farC = swap ? n.c[2] : n.c[3];
-        stack[sp * YRT_TRACE_BLOCK] = (farI << 5) | farC;
+        const int e = (farI << 5) | farC;
+        if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
+        else spill[sp - YRT_LDS_STACK] = e;
         sp += 1;
         curIdx = nearI;
         curCnt = nearC;
@@ -123,30 +133,30 @@ __device__ __forceinline__ Hit traverse(const GpuNode* __restrict__ nodes, const
     } else {
       for (int i = 0; i < curCnt; ++i) {
         const GpuTri tr = tris[curIdx + i];
-        float t, u, v;
-        bool ok = tri_test(tr, r, ANY ? r.tfar : best.t + 0.0f, t, u, v);
+        float t, U, V, absDen;
+        bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
         int gid = __float_as_int(tr.v0[3]);
         if (ANY) {
           if (ok) {
-            best.t = t; best.u = u; best.v = v; best.tri = gid;
+            best.t = t; best.u = U / absDen; best.v = V / absDen; best.tri = gid;
             return best;
           }
         } else {
           // strict (t < best) or tie with smaller id; tri_test used tfar = best.t so ties
           // (t == best.t) were rejected: re-test them against the original tfar.
           if (!ok && best.tri >= 0 && t == best.t && gid < best.tri) {
-            float t2, u2, v2;
-            ok = tri_test(tr, r, r.tfar, t2, u2, v2);
+            float t2, U2, V2, a2;
+            ok = tri_test_t(tr, r, r.tfar, t2, U2, V2, a2);
           }
           if (ok) {
-            best.t = t; best.u = u; best.v = v; best.tri = gid;
+            best.t = t; best.u = U / absDen; best.v = V / absDen; best.tri = gid;
           }
         }
       }
     }
     if (sp == 0) break;
     sp -= 1;
-    const int e = stack[sp * YRT_TRACE_BLOCK];
+    const int e = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK];
     curIdx = e >> 5;
     curCnt = e & 31;
   }
