@@ -261,29 +261,147 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
   }
 }
 
+// Ray-query kernel with lane refill (persistent-wave traversal, after Aila & Laine 2009):
+// each wave owns a contiguous chunk of the queue; the traversal advances one node visit or
+// one leaf per iteration, and whenever at least YRT_REFILL lanes of the wave have finished
+// their ray, those lanes take the next rays of the chunk (ballot + popcount, no atomics).
+// This keeps 64-wide waves busy although ray costs differ by 10-100x. Same visit order and
+// the same (t, triangle id) closest-hit rule as traverse<>.
+#ifndef YRT_REFILL
+#define YRT_REFILL 16
+#endif
 template <bool ANY>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
                                                          int* __restrict__ occOut) {
-  __shared__ int stack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
+  __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
-  const int n = (int)qm.pre[YRT_QSEGS];
-  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    if (base + (int)threadIdx.x >= n) break;
-    const int q = qmap_phys(qm, segCap, (unsigned)(base + threadIdx.x));
-    const float4 o = org[q], d = dir[q];
-    RayPre r;
-    r.org = v3(o.x, o.y, o.z);
-    r.dir = v3(d.x, d.y, d.z);
-    r.inv = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-    r.tnear = o.w;
-    r.tfar = d.w;
-    const Hit h = traverse<ANY>(sv.nodes, sv.tris, r, stack + threadIdx.x);
-    if (ANY) occOut[q] = h.tri >= 0 ? 1 : 0;
-    else hitOut[q] = make_float4(h.t, h.u, h.v, __int_as_float(h.tri));
+  const unsigned n = qm.pre[YRT_QSEGS];
+  const int lane = lane_id();
+  const unsigned wavesPerBlock = YRT_TRACE_BLOCK / 64;
+  const unsigned gw = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
+  const unsigned numWaves = gridDim.x * wavesPerBlock;
+  unsigned chunk = (n + numWaves - 1) / numWaves;
+  chunk = chunk < 64u ? 64u : chunk;
+  unsigned next = gw * chunk;
+  const unsigned end = min(n, next + chunk);
+  if (next >= end) return;  // wave-uniform
+
+  const GpuNode* __restrict__ nodes = sv.nodes;
+  const GpuTri* __restrict__ tris = sv.tris;
+  int* stack = lstack + threadIdx.x;
+  int spill[YRT_STACK_DEPTH > YRT_LDS_STACK ? YRT_STACK_DEPTH - YRT_LDS_STACK : 1];
+
+  bool has = false;
+  int q = 0, sp = 0, curIdx = 0, curCnt = 0;
+  RayPre r;
+  r.org = r.dir = r.inv = v3s(0.f);
+  r.tnear = r.tfar = 0.f;
+  Hit best;
+  best.t = best.u = best.v = 0.f;
+  best.tri = -1;
+  const unsigned long long ltMask = (1ull << lane) - 1ull;
+
+  while (true) {
+    const unsigned long long idle = __ballot(!has);
+    const int nIdle = __popcll(idle);
+    if (nIdle >= YRT_REFILL) {
+      if (next < end) {
+        if (!has) {
+          const unsigned li = next + (unsigned)__popcll(idle & ltMask);
+          if (li < end) {
+            q = qmap_phys(qm, segCap, li);
+            const float4 o = org[q], d = dir[q];
+            r.org = v3(o.x, o.y, o.z);
+            r.dir = v3(d.x, d.y, d.z);
+            r.inv = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
+            r.tnear = o.w;
+            r.tfar = d.w;
+            best.t = r.tfar;
+            best.u = best.v = 0.f;
+            best.tri = -1;
+            sp = 0;
+            curIdx = 0;
+            curCnt = 0;
+            // NaN tfar (tMaxShadowRay = inf): no hit, nothing to traverse
+            has = r.tfar >= r.tnear;
+            if (!has) {
+              if (ANY) occOut[q] = 0;
+              else hitOut[q] = make_float4(best.t, 0.f, 0.f, __int_as_float(-1));
+            }
+          }
+        }
+        next += (unsigned)nIdle;
+      } else if (nIdle == 64) {
+        break;
+      }
+    }
+    if (!has) continue;
+
+    bool pop = true;
+    if (curCnt == 0) {
+      const GpuNode nd = nodes[curIdx];
+      bool h0, h1;
+      float t0, t1;
+      box2(nd, r, best.t, h0, h1, t0, t1);
+      if (h0 && h1) {
+        const bool swap = t1 < t0;
+        const int farI = swap ? nd.c[0] : nd.c[1], farC = swap ? nd.c[2] : nd.c[3];
+        const int e = (farI << 5) | farC;
+        if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
+        else spill[sp - YRT_LDS_STACK] = e;
+        sp += 1;
+        curIdx = swap ? nd.c[1] : nd.c[0];
+        curCnt = swap ? nd.c[3] : nd.c[2];
+        pop = false;
+      } else if (h0 || h1) {
+        curIdx = h0 ? nd.c[0] : nd.c[1];
+        curCnt = h0 ? nd.c[2] : nd.c[3];
+        pop = false;
+      }
+    } else {
+      bool found = false;
+      for (int i = 0; i < curCnt; ++i) {
+        const GpuTri tr = tris[curIdx + i];
+        float t, U, V, absDen;
+        bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
+        const int gid = __float_as_int(tr.v0[3]);
+        if (ANY) {
+          if (ok) {
+            found = true;
+            break;
+          }
+        } else {
+          if (!ok && best.tri >= 0 && t == best.t && gid < best.tri) {
+            float t2, U2, V2, a2;
+            ok = tri_test_t(tr, r, r.tfar, t2, U2, V2, a2);
+          }
+          if (ok) {
+            best.t = t; best.u = U / absDen; best.v = V / absDen; best.tri = gid;
+          }
+        }
+      }
+      if (ANY && found) {
+        occOut[q] = 1;
+        has = false;
+        continue;
+      }
+    }
+    if (pop) {
+      if (sp == 0) {
+        if (ANY) occOut[q] = 0;
+        else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
+        has = false;
+      } else {
+        sp -= 1;
+        const int e = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK];
+        curIdx = e >> 5;
+        curCnt = e & 31;
+      }
+    }
   }
 }
 
@@ -837,6 +955,11 @@ __global__ __launch_bounds__(64) void k_debug(SceneView sv, FrameView fv, int ma
 }
 
 // ---------------------------------------------------------------- launchers
+// Trace grid: 256 CUs x 8 waves/SIMD x 4 SIMDs = 8192 resident waves = 4096 blocks of 128;
+// twice that so a CU always has a queued block when one drains.
+#ifndef YRT_TRACE_GRID
+#define YRT_TRACE_GRID 8192
+#endif
 static inline int grid_for(long long n, int block, int maxBlocks) {
   long long g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -857,15 +980,15 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
                           int numSegs, int segCap, float4* hit, hipStream_t s) {
   const long long maxCount = (long long)numSegs * segCap;
-  hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
-                     sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr);
+  hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
+                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr);
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s) {
   const long long maxCount = (long long)numSegs * segCap;
-  hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, 256 * 64)), dim3(YRT_TRACE_BLOCK), 0, s,
-                     sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded);
+  hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
+                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded);
 }
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
