@@ -296,7 +296,20 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
   int spill[YRT_STACK_DEPTH > YRT_LDS_STACK ? YRT_STACK_DEPTH - YRT_LDS_STACK : 1];
 
   bool has = false;
-  int q = 0, sp = 0, curIdx = 0, curCnt = 0;
+  // cur: next entry to process (count 0 = inner node, >0 = leaf range, -1 = stack exhausted)
+  // pend: a leaf parked during the inner-node phase (count 0 = none)
+  int q = 0, sp = 0, curIdx = 0, curCnt = 0, pendIdx = 0, pendCnt = 0;
+#define YRT_POP()                                                                                   \
+  do {                                                                                              \
+    if (sp == 0) {                                                                                  \
+      curCnt = -1;                                                                                  \
+    } else {                                                                                        \
+      sp -= 1;                                                                                      \
+      const int e_ = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK]; \
+      curIdx = e_ >> 5;                                                                             \
+      curCnt = e_ & 31;                                                                             \
+    }                                                                                               \
+  } while (0)
   RayPre r;
   r.org = r.dir = r.inv = v3s(0.f);
   r.tnear = r.tfar = 0.f;
@@ -326,6 +339,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
             sp = 0;
             curIdx = 0;
             curCnt = 0;
+            pendCnt = 0;
             // NaN tfar (tMaxShadowRay = inf): no hit, nothing to traverse
             has = r.tfar >= r.tnear;
             if (!has) {
@@ -341,40 +355,58 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
     }
     if (!has) continue;
 
-    bool pop = true;
-    if (curCnt == 0) {
-      const GpuNode nd = nodes[curIdx];
-      bool h0, h1;
-      float t0, t1;
-      box2(nd, r, best.t, h0, h1, t0, t1);
-      if (h0 && h1) {
-        const bool swap = t1 < t0;
-        const int farI = swap ? nd.c[0] : nd.c[1], farC = swap ? nd.c[2] : nd.c[3];
-        const int e = (farI << 5) | farC;
-        if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
-        else spill[sp - YRT_LDS_STACK] = e;
-        sp += 1;
-        curIdx = swap ? nd.c[1] : nd.c[0];
-        curCnt = swap ? nd.c[3] : nd.c[2];
-        pop = false;
-      } else if (h0 || h1) {
-        curIdx = h0 ? nd.c[0] : nd.c[1];
-        curCnt = h0 ? nd.c[2] : nd.c[3];
-        pop = false;
+    // ---- inner-node phase ("while-while" with speculative leaf postponing, Aila & Laine
+    // 2009): a lane that reaches a leaf parks it in pend* and keeps descending; the phase
+    // ends when every traversing lane holds a parked leaf or no lane is at an inner node.
+    while (true) {
+      if (curCnt == 0) {
+        const GpuNode nd = nodes[curIdx];
+        bool h0, h1;
+        float t0, t1;
+        box2(nd, r, best.t, h0, h1, t0, t1);
+        if (h0 && h1) {
+          const bool swap = t1 < t0;
+          const int farI = swap ? nd.c[0] : nd.c[1], farC = swap ? nd.c[2] : nd.c[3];
+          const int e = (farI << 5) | farC;
+          if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
+          else spill[sp - YRT_LDS_STACK] = e;
+          sp += 1;
+          curIdx = swap ? nd.c[1] : nd.c[0];
+          curCnt = swap ? nd.c[3] : nd.c[2];
+        } else if (h0 || h1) {
+          curIdx = h0 ? nd.c[0] : nd.c[1];
+          curCnt = h0 ? nd.c[2] : nd.c[3];
+        } else {
+          YRT_POP();
+        }
+        if (curCnt > 0 && pendCnt == 0) {
+          pendIdx = curIdx;
+          pendCnt = curCnt;
+          YRT_POP();
+        }
       }
-    } else {
-      bool found = false;
-      for (int i = 0; i < curCnt; ++i) {
-        const GpuTri tr = tris[curIdx + i];
+      if (!__any(curCnt == 0)) break;
+      if (!__any(curCnt == 0 && pendCnt == 0)) break;
+    }
+
+    // ---- leaf phase: the parked leaf, then the current entry if it is a leaf too
+    bool found = false;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+      int lIdx = pendIdx, lCnt = pendCnt;
+      if (pass == 1) {
+        lIdx = curIdx;
+        lCnt = curCnt > 0 ? curCnt : 0;
+      }
+      for (int i = 0; i < lCnt && !found; ++i) {
+        const GpuTri tr = tris[lIdx + i];
         float t, U, V, absDen;
         bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
         const int gid = __float_as_int(tr.v0[3]);
         if (ANY) {
-          if (ok) {
-            found = true;
-            break;
-          }
+          found = ok;
         } else {
+          // ties (t == best.t) were rejected by the strict test: smaller id wins
           if (!ok && best.tri >= 0 && t == best.t && gid < best.tri) {
             float t2, U2, V2, a2;
             ok = tri_test_t(tr, r, r.tfar, t2, U2, V2, a2);
@@ -384,23 +416,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
           }
         }
       }
-      if (ANY && found) {
-        occOut[q] = 1;
-        has = false;
-        continue;
-      }
+      if (pass == 0) pendCnt = 0;
+      else if (curCnt > 0) YRT_POP();
     }
-    if (pop) {
-      if (sp == 0) {
-        if (ANY) occOut[q] = 0;
-        else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
-        has = false;
-      } else {
-        sp -= 1;
-        const int e = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK];
-        curIdx = e >> 5;
-        curCnt = e & 31;
-      }
+    if (ANY && found) {
+      occOut[q] = 1;
+      has = false;
+    } else if (curCnt < 0) {
+      if (ANY) occOut[q] = 0;
+      else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
+      has = false;
     }
   }
 }
