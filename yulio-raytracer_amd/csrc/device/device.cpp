@@ -80,7 +80,7 @@ class Device {
 
   // per-frame device state
   DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCounters, dCount;
-  DevBuf qPath[2], qOrg[2], qDir[2], hit, thr, L, meta, shFirst, sOrg, sDir, sContrib, sOcc;
+  DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], qL[2], qNext, hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc;
   int64_t pathCap = 0, shadowCap = 0;
   FrameCache fcache;
   std::vector<hipEvent_t> eventPool;
@@ -125,11 +125,12 @@ class Device {
         qPath[k].alloc(Q * 4);
         qOrg[k].alloc(Q * 16);
         qDir[k].alloc(Q * 16);
+        qThr[k].alloc(Q * 16);
+        qL[k].alloc(Q * 16);
       }
+      qNext.alloc(Q * 4);
       hit.alloc(Q * 16);
-      thr.alloc(Q * 16);
-      L.alloc(Q * 16);
-      meta.alloc(Q * 4);
+      pathL.alloc(Q * 16);
       pathCap = Q;
     }
     const int64_t S = Q * std::max(1, numLights);
@@ -270,10 +271,13 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
       pb.qOrg[k] = qOrg[k].as<float4>();
       pb.qDir[k] = qDir[k].as<float4>();
     }
+    for (int k = 0; k < 2; ++k) {
+      pb.qThr[k] = qThr[k].as<float4>();
+      pb.qL[k] = qL[k].as<float4>();
+    }
+    pb.qNext = qNext.as<int>();
     pb.hit = hit.as<float4>();
-    pb.thr = thr.as<float4>();
-    pb.L = L.as<float4>();
-    pb.meta = meta.as<int>();
+    pb.pathL = pathL.as<float4>();
     pb.shFirst = shFirst.as<int>();
     pb.sOrg = sOrg.as<float4>();
     pb.sDir = sDir.as<float4>();

@@ -237,15 +237,13 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       const int s = p / bi.numPixels, i = p - s * bi.numPixels;
       int x, y;
       valid = batch_pixel(rp, bi, i, x, y);
-      pb.L[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pb.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
         const int set = fv.pixelSets[(size_t)y * rp.width + x];
         const int rec = set * rp.spp + s;
         const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
         const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
         camera_ray(cam, fx, fy, org, dir);
-        pb.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);
-        pb.meta[p] = (0) | (0 << 8) | (1 << 9);
       }
       // loop head of Li: depth < maxDepth and max(throughput)=1 >= minContribution
       valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
@@ -257,6 +255,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       pb.qPath[0][q] = p;
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
       pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
+      pb.qThr[0][q] = make_float4(1.f, 1.f, 1.f, __int_as_float((0) | (0 << 8) | (1 << 9)));
+      pb.qL[0][q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -704,10 +704,10 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
       org = v3(o.x, o.y, o.z);
       dir = v3(d.x, d.y, d.z);
       h = pb.hit[q];
-      const float4 t4 = pb.thr[path], l4 = pb.L[path];
+      const float4 t4 = pb.qThr[cur][q], l4 = pb.qL[cur][q];
       thr = v3(t4.x, t4.y, t4.z);
       L = v3(l4.x, l4.y, l4.z);
-      meta = pb.meta[path];
+      meta = __float_as_int(t4.w);
       depth = meta & 255;
       ignoreVL = (meta >> 8) & 1;
       unbent = (meta >> 9) & 1;
@@ -743,7 +743,6 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
         for (int k = 0; k < YRT_MAX_COMPS; ++k)
           if (k < bs.n) useDirect |= (bs.c[k].type & BT_DIFFUSE) != 0;
       }
-      pb.L[path] = make_float4(L.x, L.y, L.z, 0.f);
     }
 
     // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167)
@@ -796,7 +795,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
 
     // continuation (pathtraceintegrator.cpp:169-213)
     bool cont = false;
-    V3 nwi = v3s(0.f);
+    V3 nwi = v3s(0.f), nthr = v3s(0.f);
+    int nmeta = 0;
     if (active && isHit) {
       bool stop = depth >= rp.maxDepth - 1;
       if (!stop && rp.rrDepth > 0 && depth >= rp.rrDepth - 1) {  // size_t compare in the reference
@@ -812,14 +812,13 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
         uint32_t type;
         const V3 c = set_sample(bs, wo, dg, sx, sy, ss, nwi, pdf, type);
         if (!(c == v3s(0.f) || pdf <= 0.f)) {
-          const V3 nthr = thr * c * rcpf_(pdf);
+          nthr = thr * c * rcpf_(pdf);
           const bool nIgnore = (type & BT_DIFFUSE) != 0;
           const bool nUnbent = unbent && (nwi == dir);
           // loop head of the next iteration: depth+1 < maxDepth holds; minContribution test
           if (!(reduce_max(nthr) < rp.minContribution)) {
             cont = true;
-            pb.thr[path] = make_float4(nthr.x, nthr.y, nthr.z, 0.f);
-            pb.meta[path] = (depth + 1) | ((nIgnore ? 1 : 0) << 8) | ((nUnbent ? 1 : 0) << 9);
+            nmeta = (depth + 1) | ((nIgnore ? 1 : 0) << 8) | ((nUnbent ? 1 : 0) << 9);
           }
         }
       }
@@ -830,7 +829,12 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
       pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
+      pb.qThr[cur ^ 1][nq] = make_float4(nthr.x, nthr.y, nthr.z, __int_as_float(nmeta));
+      pb.qL[cur ^ 1][nq] = make_float4(L.x, L.y, L.z, 0.f);
+    } else if (active) {
+      pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);  // path ends here
     }
+    if (active) pb.qNext[q] = got ? (int)nq : -1;
   }
 }
 
@@ -845,8 +849,10 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, in
     bool any = false;
     for (int li = 0; li < numLights; ++li) any |= pb.shFirst[(size_t)q * numLights + li] >= 0;
     if (!any) continue;
-    const int path = pb.qPath[cur][q];
-    const float4 l4 = pb.L[path];
+    // the path's radiance now lives in the next queue (continued) or in pathL (ended)
+    const int nq = pb.qNext[q];
+    float4* Lp = nq >= 0 ? &pb.qL[cur ^ 1][nq] : &pb.pathL[pb.qPath[cur][q]];
+    const float4 l4 = *Lp;
     V3 L = v3(l4.x, l4.y, l4.z);
     for (int li = 0; li < numLights; ++li) {
       const int si = pb.shFirst[(size_t)q * numLights + li];
@@ -854,7 +860,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, in
       const float4 c = pb.sContrib[si];
       L = L + v3(c.x, c.y, c.z);
     }
-    pb.L[path] = make_float4(L.x, L.y, L.z, 0.f);
+    *Lp = make_float4(L.x, L.y, L.z, 0.f);
   }
 }
 
@@ -869,7 +875,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
     if (!batch_pixel(rp, bi, i, x, y)) continue;
     V3 L = v3s(0.f);
     for (int s = 0; s < rp.spp; ++s) {
-      const float4 l4 = pb.L[(size_t)s * bi.numPixels + i];
+      const float4 l4 = pb.pathL[(size_t)s * bi.numPixels + i];
       L = L + v3(l4.x, l4.y, l4.z);
     }
     // AccuBuffer::update: non-accumulating frames store (L, spp), accumulating ones add

@@ -55,15 +55,18 @@ inline __host__ __device__ int qseg_capacity(long long items) {
 }
 
 // Wavefront state for one batch of P = numPixels * spp paths (SoA, device memory).
+// Path state travels with the queue entry (coalesced in queue order); only the final
+// radiance is scattered to the path-indexed pathL, once, when a path terminates.
 struct PathBuffers {
   int* qPath[2];
   float4* qOrg[2];   // xyz, tnear
   float4* qDir[2];   // xyz, tfar
-  float4* hit;       // t, u, v, tri (bits)
-  float4* thr;       // per path throughput
-  float4* L;         // per path radiance
-  int* meta;         // per path: depth | ignoreVL<<8 | unbent<<9
-  int* shFirst;      // per (queue entry, light): shadow-ray slot or -1
+  float4* qThr[2];   // throughput xyz, w = meta bits: depth | ignoreVL<<8 | unbent<<9
+  float4* qL[2];     // radiance so far (xyz)
+  int* qNext;        // per closest-queue slot: slot of the continuation in the next queue, -1 = ended
+  float4* hit;       // t, u, v, tri (bits), per closest-queue slot
+  float4* pathL;     // per path id: final radiance
+  int* shFirst;      // per (queue slot, light): shadow-ray slot or -1
   float4* sOrg;      // shadow rays
   float4* sDir;
   float4* sContrib;
