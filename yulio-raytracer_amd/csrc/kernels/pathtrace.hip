@@ -432,7 +432,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
 
 // ---------------------------------------------------------------- shading helpers
 // BackendSceneFlat::postIntersect -> Shape::postIntersect
-__device__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
+__device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
                                bool wantTangents) {
   const int g = sv.triGeom[gid];
   const GpuGeom geom = sv.geoms[g];
@@ -506,19 +506,23 @@ __device__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, flo
 
 __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V3 R, float a = 0.f, float b = 0.f,
                                          float c = 0.f) {
-  if (bs.n < YRT_MAX_COMPS) {
-    Comp& k = bs.c[bs.n++];
-    k.kind = kind;
-    k.type = type;
-    k.R = R;
-    k.a = a;
-    k.b = b;
-    k.c = c;
+  // Unconditional constant-index stores of selected values: a conditional store lets the
+  // optimizer merge the slots into a pointer phi, which pins the set in scratch memory.
+#pragma unroll
+  for (int i = 0; i < YRT_MAX_COMPS; ++i) {
+    const bool w = i == bs.n;
+    bs.c[i].kind = w ? kind : bs.c[i].kind;
+    bs.c[i].type = w ? type : bs.c[i].type;
+    bs.c[i].R = v3(w ? R.x : bs.c[i].R.x, w ? R.y : bs.c[i].R.y, w ? R.z : bs.c[i].R.z);
+    bs.c[i].a = w ? a : bs.c[i].a;
+    bs.c[i].b = w ? b : bs.c[i].b;
+    bs.c[i].c = w ? c : bs.c[i].c;
   }
+  bs.n = bs.n < YRT_MAX_COMPS ? bs.n + 1 : bs.n;
 }
 
 // Material::shade for the in-scope materials (materials/*.h). May modify dg.Ns (Obj bump).
-__device__ void shade_material(const SceneView& sv, const GpuMaterial& m, DG& dg, BRDFSet& bs) {
+__device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, DG& dg, BRDFSet& bs) {
   bs.n = 0;
   switch (m.type) {
     case MAT_MATTE:
@@ -608,7 +612,7 @@ __device__ __forceinline__ void img_get(const SceneView& sv, int image, int x, i
 }
 
 // HDRILight::Le (lights/hdrilight.cpp:43-71)
-__device__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
+__device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
   const A3 w2l = ldA3(lt.w2l);
   const V3 wi = xfmVector(w2l, -wo);
   const float theta = acosf(clampf(wi.y, -1.0f, 1.0f));
@@ -647,7 +651,7 @@ __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3
 }
 
 // Light::sample for a non-precomputed light; returns L, sets wi/pdf.
-__device__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
+__device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
   if (lt.type == LIGHT_AMBIENT) {
     // lights/ambientlight.h:52-65 (the bsphere tMax is overwritten by the integrator)
     wi = cosine_hemi(sx, sy, dg.Ns, pdf);
@@ -674,7 +678,12 @@ __device__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy,
   return v3s(0.f);
 }
 
-__global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
+// Occupancy target for k_shade: 3 waves/SIMD caps it at 168 VGPRs with a few bytes of spill
+// (unconstrained it takes 183 VGPRs = 2 waves/SIMD).
+#ifndef YRT_SHADE_WAVES
+#define YRT_SHADE_WAVES 3
+#endif
+__global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
   const GpuRenderParams& rp = *fv.rp;
   __shared__ QMap qm;
@@ -697,6 +706,13 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
     DG dg;
     BRDFSet bs;
     bs.n = 0;
+#pragma unroll
+    for (int k = 0; k < YRT_MAX_COMPS; ++k) {
+      bs.c[k].kind = 0;
+      bs.c[k].type = 0;
+      bs.c[k].R = v3s(0.f);
+      bs.c[k].a = bs.c[k].b = bs.c[k].c = 0.f;
+    }
     V3 wo = v3s(0.f);
     if (active) {
       path = pb.qPath[cur][q];
@@ -740,6 +756,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
           const GpuLight& al = sv.lights[dg.light];
           L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
         }
+#pragma unroll
         for (int k = 0; k < YRT_MAX_COMPS; ++k)
           if (k < bs.n) useDirect |= (bs.c[k].type & BT_DIFFUSE) != 0;
       }
@@ -751,7 +768,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shade(SceneView sv, FrameView fv,
       V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
       float tnear = 0.f, tfar = 0.f;
       if (active && isHit && useDirect) {
-        const GpuLight lt = sv.lights[li];
+        const GpuLight& lt = sv.lights[li];
         if ((lt.illumMask & dg.illumMask) != 0) {
           V3 Ls;
           float pdf;

@@ -200,7 +200,7 @@ __device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, 
   return c.R * (c.a + 2) * (1.0f / (2.0f * kPi)) * powf(dot(r, wi), c.a) * clampf(dot(wi, dg.Ns));
 }
 
-__device__ __forceinline__ V3 comp_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+__device__ __forceinline__ V3 comp_eval(const Comp c, V3 wo, const DG& dg, V3 wi) {
   switch (c.kind) {
     case C_LAMBERT: return lambert_eval(c.R, dg, wi);
     case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
@@ -211,7 +211,7 @@ __device__ __forceinline__ V3 comp_eval(const Comp& c, V3 wo, const DG& dg, V3 w
 }
 
 // BRDF::sample of one component; returns color, sets wi/pdf.
-__device__ __forceinline__ V3 comp_sample(const Comp& c, V3 wo, const DG& dg, float sx, float sy, V3& wi,
+__device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, float sx, float sy, V3& wi,
                                           float& pdf) {
   switch (c.kind) {
     case C_LAMBERT: {
@@ -303,34 +303,49 @@ __device__ __forceinline__ V3 comp_sample(const Comp& c, V3 wo, const DG& dg, fl
 // CompositedBRDF::eval restricted to `type` (compositedbrdf.h:59-65)
 __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V3 wi, uint32_t type) {
   V3 c = v3s(0.0f);
+#pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i)
-    if (i < bs.n && (bs.c[i].type & type)) c = c + comp_eval(bs.c[i], wo, dg, wi);
+    if (i < bs.n && (bs.c[i].type & type)) {
+      const Comp ci = bs.c[i];
+      c = c + comp_eval(ci, wo, dg, wi);
+    }
   return c;
 }
 
-// CompositedBRDF::sample (compositedbrdf.h:104-166)
+// CompositedBRDF::sample (compositedbrdf.h:104-166). Same arithmetic as the reference
+// (f_i = sum(c_i)/pdf_i over the components that sampled something, normalized by their
+// running sum, CDF with the last entry forced to 1), written with compile-time component
+// indices only so nothing is spilled to scratch.
 __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg, float sx, float sy, float ss,
                                          V3& wi_o, float& pdf_o, uint32_t& type_o) {
   float f[YRT_MAX_COMPS];
   V3 colors[YRT_MAX_COMPS];
   V3 dirs[YRT_MAX_COMPS];
   float pdfs[YRT_MAX_COMPS];
-  uint32_t types[YRT_MAX_COMPS];
+  bool ok[YRT_MAX_COMPS];
   float sum = 0.0f;
   int num = 0;
+#pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i) {
-    if (i >= bs.n) break;
-    V3 wi;
-    float pdf = 0.0f;
-    V3 c = comp_sample(bs.c[i], wo, dg, sx, sy, wi, pdf);
-    if ((c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) || pdf <= 0.0f) continue;
-    f[num] = (c.x + c.y + c.z) * rcpf_(pdf);
-    sum += f[num];
-    colors[num] = c;
-    dirs[num] = wi;
-    pdfs[num] = pdf;
-    types[num] = bs.c[i].type;
-    num++;
+    ok[i] = false;
+    f[i] = 0.0f;
+    pdfs[i] = 0.0f;
+    colors[i] = dirs[i] = v3s(0.0f);
+    if (i < bs.n) {
+      V3 wi;
+      float pdf = 0.0f;
+      const Comp ci = bs.c[i];
+      const V3 c = comp_sample(ci, wo, dg, sx, sy, wi, pdf);
+      if (!((c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) || pdf <= 0.0f)) {
+        ok[i] = true;
+        f[i] = (c.x + c.y + c.z) * rcpf_(pdf);
+        sum += f[i];
+        colors[i] = c;
+        dirs[i] = wi;
+        pdfs[i] = pdf;
+        num++;
+      }
+    }
   }
   if (num == 0) {
     wi_o = v3s(0.0f);
@@ -338,17 +353,34 @@ __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg,
     type_o = 0;
     return v3s(0.0f);
   }
-  for (int i = 0; i < num; ++i) f[i] /= sum;
-  float d[YRT_MAX_COMPS];
-  d[0] = f[0];
-  for (int i = 1; i < num - 1; ++i) d[i] = d[i - 1] + f[i];
-  d[num - 1] = 1.0f;
-  int i = 0;
-  while (i < num - 1 && ss > d[i]) i++;
-  wi_o = dirs[i];
-  pdf_o = pdfs[i] * f[i];
-  type_o = types[i];
-  return colors[i];
+  // choose the first valid component k (in order) with !(ss > d_k); the last one has d = 1
+  float d = 0.0f;
+  int k = 0;  // index among valid components
+  int chosen = -1;
+#pragma unroll
+  for (int i = 0; i < YRT_MAX_COMPS; ++i) {
+    if (ok[i]) {
+      const float fi = f[i] / sum;
+      f[i] = fi;
+      d = (k == 0) ? fi : d + fi;
+      const float dk = (k == num - 1) ? 1.0f : d;
+      if (chosen < 0 && (k == num - 1 || !(ss > dk))) chosen = i;
+      k++;
+    }
+  }
+  V3 col = colors[0];
+  wi_o = dirs[0];
+  pdf_o = pdfs[0] * f[0];
+  type_o = bs.c[0].type;
+#pragma unroll
+  for (int i = 1; i < YRT_MAX_COMPS; ++i)
+    if (chosen == i) {
+      col = colors[i];
+      wi_o = dirs[i];
+      pdf_o = pdfs[i] * f[i];
+      type_o = bs.c[i].type;
+    }
+  return col;
 }
 
 }  // namespace yrt

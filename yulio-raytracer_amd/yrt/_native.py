@@ -11,7 +11,8 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_DIR = Path(__file__).resolve().parent.parent / "lib"
+# YRT_LIB_DIR selects an alternative in-tree build (e.g. a tuning variant under lib_variants/)
+LIB_DIR = Path(os.environ.get("YRT_LIB_DIR", Path(__file__).resolve().parent.parent / "lib"))
 DEVICE_LIB = LIB_DIR / "libdevice_singleray_mi355x.so"
 FRONTEND_LIB = LIB_DIR / "libYulioRT_mi355x.so"
 
