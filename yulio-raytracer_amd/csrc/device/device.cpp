@@ -144,6 +144,12 @@ class Device {
     }
   }
 
+  DevBuf dSpill;  // deep traversal-stack entries of k_trace (rarely touched)
+  int* spill() {
+    dSpill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
+    return dSpill.as<int>();
+  }
+
   hipEvent_t ev() {
     hipEvent_t e;
     HIP_CHECK(hipEventCreate(&e));
@@ -168,6 +174,8 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
   if (!S.gpu) throw std::runtime_error("scene not committed");
   if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
   GpuScene& G = *S.gpu;
+  SceneView sv = G.view;
+  sv.traceSpill = spill();
   const int W = F.width, H = F.height;
   memset(&stats, 0, sizeof(stats));
 
@@ -303,19 +311,19 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         const int cur = d & 1;
         EvPair e1{};
         if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, stream)); }
-        launch_trace_closest(G.view, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
+        launch_trace_closest(sv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
                              pb.segCap, pb.hit, stream);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, stream)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
           capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap);
         EvPair e2{};
         if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
-        launch_shade(G.view, fv, pb, bi, d, stream);
+        launch_shade(sv, fv, pb, bi, d, stream);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, stream)); evs.push_back(e2); }
         if (rp.numLights > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
-          launch_trace_any(G.view, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
+          launch_trace_any(sv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
                            pb.sOcc, stream);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
@@ -389,10 +397,12 @@ void Device::intersect(SceneObj& S, const float* org4, const float* dir4, uint32
   if (!S.gpu) throw std::runtime_error("scene not committed");
   dCount.alloc(sizeof(unsigned));
   HIP_CHECK(hipMemcpyAsync(dCount.p, &n, sizeof(unsigned), hipMemcpyHostToDevice, st));
+  SceneView sv = S.gpu->view;
+  sv.traceSpill = spill();
   if (occ)
-    launch_trace_any(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n, occ, st);
+    launch_trace_any(sv, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n, occ, st);
   else
-    launch_trace_closest(S.gpu->view, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n,
+    launch_trace_closest(sv, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n,
                          (float4*)hit4, st);
   HIP_CHECK(hipStreamSynchronize(st));
 }

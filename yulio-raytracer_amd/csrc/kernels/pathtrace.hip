@@ -275,7 +275,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
-                                                         int* __restrict__ occOut) {
+                                                         int* __restrict__ occOut, int* __restrict__ spillBuf) {
   __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
@@ -293,22 +293,36 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
   const GpuNode* __restrict__ nodes = sv.nodes;
   const GpuTri* __restrict__ tris = sv.tris;
   int* stack = lstack + threadIdx.x;
-  int spill[YRT_STACK_DEPTH > YRT_LDS_STACK ? YRT_STACK_DEPTH - YRT_LDS_STACK : 1];
+  // Deep stack entries (rare) spill to global memory, [entry][thread]: a private array here
+  // would let the compiler fuse LDS and scratch pops into one slow flat load.
+  const size_t spillStride = (size_t)gridDim.x * YRT_TRACE_BLOCK;
+  int* __restrict__ spill = spillBuf + blockIdx.x * YRT_TRACE_BLOCK + threadIdx.x;
 
   bool has = false;
   // cur: next entry to process (count 0 = inner node, >0 = leaf range, -1 = stack exhausted)
   // pend: a leaf parked during the inner-node phase (count 0 = none)
   int q = 0, sp = 0, curIdx = 0, curCnt = 0, pendIdx = 0, pendCnt = 0;
-#define YRT_POP()                                                                                   \
-  do {                                                                                              \
-    if (sp == 0) {                                                                                  \
-      curCnt = -1;                                                                                  \
-    } else {                                                                                        \
-      sp -= 1;                                                                                      \
-      const int e_ = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK]; \
-      curIdx = e_ >> 5;                                                                             \
-      curCnt = e_ & 31;                                                                             \
-    }                                                                                               \
+  // The LDS stack is a ring holding the top YRT_LDS_STACK entries; older entries are evicted
+  // to global memory on push and restored into the freed slot on pop (both rare). Every pop
+  // returns an LDS value, so the hot path stays a ds_read.
+#define YRT_SLOT(i) ((((i) & (YRT_LDS_STACK - 1))) * YRT_TRACE_BLOCK)
+#define YRT_PUSH(e)                                                               \
+  do {                                                                            \
+    if (sp >= YRT_LDS_STACK) spill[(size_t)(sp - YRT_LDS_STACK) * spillStride] = stack[YRT_SLOT(sp)]; \
+    stack[YRT_SLOT(sp)] = (e);                                                    \
+    sp += 1;                                                                      \
+  } while (0)
+#define YRT_POP()                                                                 \
+  do {                                                                            \
+    if (sp == 0) {                                                                \
+      curCnt = -1;                                                                \
+    } else {                                                                      \
+      sp -= 1;                                                                    \
+      const int e_ = stack[YRT_SLOT(sp)];                                         \
+      if (sp >= YRT_LDS_STACK) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - YRT_LDS_STACK) * spillStride]; \
+      curIdx = e_ >> 5;                                                           \
+      curCnt = e_ & 31;                                                           \
+    }                                                                             \
   } while (0)
   RayPre r;
   r.org = r.dir = r.inv = v3s(0.f);
@@ -364,18 +378,15 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
         bool h0, h1;
         float t0, t1;
         box2(nd, r, best.t, h0, h1, t0, t1);
-        if (h0 && h1) {
-          const bool swap = t1 < t0;
-          const int farI = swap ? nd.c[0] : nd.c[1], farC = swap ? nd.c[2] : nd.c[3];
-          const int e = (farI << 5) | farC;
-          if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
-          else spill[sp - YRT_LDS_STACK] = e;
-          sp += 1;
-          curIdx = swap ? nd.c[1] : nd.c[0];
-          curCnt = swap ? nd.c[3] : nd.c[2];
-        } else if (h0 || h1) {
-          curIdx = h0 ? nd.c[0] : nd.c[1];
-          curCnt = h0 ? nd.c[2] : nd.c[3];
+        // branch-light child selection: first = nearer hit child (or the only one)
+        const bool both = h0 && h1;
+        const bool swap = both ? (t1 < t0) : !h0;
+        const int fI = swap ? nd.c[1] : nd.c[0], fC = swap ? nd.c[3] : nd.c[2];
+        const int sI = swap ? nd.c[0] : nd.c[1], sC = swap ? nd.c[2] : nd.c[3];
+        if (both) YRT_PUSH((sI << 5) | sC);
+        if (h0 || h1) {
+          curIdx = fI;
+          curCnt = fC;
         } else {
           YRT_POP();
         }
@@ -1003,11 +1014,7 @@ __global__ __launch_bounds__(64) void k_debug(SceneView sv, FrameView fv, int ma
 }
 
 // ---------------------------------------------------------------- launchers
-// Trace grid: 256 CUs x 8 waves/SIMD x 4 SIMDs = 8192 resident waves = 4096 blocks of 128;
-// twice that so a CU always has a queued block when one drains.
-#ifndef YRT_TRACE_GRID
-#define YRT_TRACE_GRID 8192
-#endif
+
 static inline int grid_for(long long n, int block, int maxBlocks) {
   long long g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1029,14 +1036,14 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
                           int numSegs, int segCap, float4* hit, hipStream_t s) {
   const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr);
+                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr, sv.traceSpill);
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s) {
   const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded);
+                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill);
 }
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,

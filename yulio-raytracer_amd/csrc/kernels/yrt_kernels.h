@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "../common/yrt_gpu_types.h"
+#include "yrt_traverse.h"
 
 namespace yrt {
 
@@ -25,8 +26,16 @@ struct SceneView {
   const GpuLight* lights;
   const int* envLights;
   const float* hdriDist;
+  int* traceSpill;   // deep traversal-stack entries: YRT_TRACE_SPILL_INTS ints
   int numLights, numEnvLights, numNodes, numTris;
 };
+
+// Trace grid: 256 CUs x 8 waves/SIMD x 4 SIMDs = 8192 resident waves = 4096 blocks of 128;
+// twice that so a CU always has a queued block when one drains.
+#ifndef YRT_TRACE_GRID
+#define YRT_TRACE_GRID 8192
+#endif
+#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * YRT_TRACE_BLOCK * (YRT_STACK_DEPTH - YRT_LDS_STACK))
 
 struct FrameView {
   const GpuRenderParams* rp;   // device copy

@@ -25,8 +25,9 @@
 #define YRT_STACK_DEPTH 64   // bound on BVH depth + 1 (device/bvh_build.cpp enforces it)
 #endif
 #ifndef YRT_LDS_STACK
-#define YRT_LDS_STACK 16     // top entries kept in LDS; deeper ones spill to per-lane scratch
+#define YRT_LDS_STACK 16     // top entries kept in LDS; deeper ones spill (power of two)
 #endif
+static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
 #define YRT_TRACE_BLOCK 128
 
 namespace yrt {
