@@ -33,7 +33,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md §HBM
-NODE_BYTES, TRI_BYTES = 64, 48  # GpuNode / GpuTri (csrc/common/yrt_gpu_types.h)
+NODE_BYTES, TRI_BYTES = 128, 48  # GpuNode (4-wide) / GpuTri (csrc/common/yrt_gpu_types.h)
 
 
 def parse():

@@ -155,7 +155,7 @@ typedef struct YRTSceneInfo {
   float bboxLo[3], bboxHi[3];
 } YRTSceneInfo;
 YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
-/* Copies the host mirror of the BVH (nodes: 64 B each, tris: 48 B each) for tests. */
+/* Copies the host mirror of the BVH (4-wide nodes: 128 B each, tris: 48 B each) for tests. */
 YRT_API int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes, void* tris,
                          size_t trisBytes);
 /* Serializes the committed scene graph + renderer + camera as the oracle's input blob

@@ -83,7 +83,7 @@ def count_visits(nodes: np.ndarray, tris: np.ndarray, org4, dir4, any_hit=False)
     n = org4.shape[0]
     nv, tv = C.c_double(), C.c_double()
     hit = np.zeros((n, 4), np.float32)
-    rc = _lib.oracle_count_visits(nodes.ctypes.data, nodes.nbytes // 64, tris.ctypes.data, tris.nbytes // 48,
+    rc = _lib.oracle_count_visits(nodes.ctypes.data, nodes.nbytes // 128, tris.ctypes.data, tris.nbytes // 48,
                                   org4.ctypes.data, dir4.ctypes.data, n, int(any_hit), C.byref(nv), C.byref(tv),
                                   hit.ctypes.data)
     if rc != 0:

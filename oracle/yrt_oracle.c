@@ -1946,9 +1946,13 @@ int oracle_scene_triangles(const void* blob, size_t bytes, float* out, int maxTr
   return n;
 }
 
-/* Device BVH node/tri layout (yulio-raytracer_amd/csrc/common/yrt_gpu_types.h), traversed in
- * the device kernel's order to count visits (SURVEY §8d algorithmic bytes). */
-typedef struct { float b0[4], b1[4], b2[4]; int32_t c[4]; } DNode;
+/* Device BVH node/tri layout (yulio-raytracer_amd/csrc/common/yrt_gpu_types.h: 4-wide 128-B
+ * nodes, 48-B triangles), traversed depth-first in the device kernel's child order (nearest
+ * hit child first, the others pushed farthest-first) to count visits for the roofline's
+ * algorithmic bytes. The wavefront kernel additionally parks one leaf while it
+ * keeps descending (speculative traversal), which can add a few node visits per ray, so
+ * these counts are a lower bound on the kernel's node fetches. */
+typedef struct { float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4]; int32_t child[4], pad[4]; } DNode;
 typedef struct { float v0[4], e1[4], e2[4]; } DTri;
 int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, size_t numTris, const float* org4,
                         const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4) {
@@ -1956,41 +1960,49 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
   const DTri* tris = (const DTri*)tris_;
   (void)numNodes; (void)numTris;
   double nv = 0, tv = 0;
+  const float INF = (float)INFINITY;
   for (int i = 0; i < n; ++i) {
     Ray r = {v3(org4[4 * i], org4[4 * i + 1], org4[4 * i + 2]), v3(dir4[4 * i], dir4[4 * i + 1], dir4[4 * i + 2]),
              org4[4 * i + 3], dir4[4 * i + 3]};
     Hit best = {r.tfar, 0, 0, -1};
     if (r.tfar >= r.tnear) {
       const V3 inv = v3(safe_inv(r.dir.x), safe_inv(r.dir.y), safe_inv(r.dir.z));
-      int stack[64], sp = 0, ci = 0, cc = 0, done = 0;
+      const float o[3] = {r.org.x, r.org.y, r.org.z}, iv[3] = {inv.x, inv.y, inv.z};
+      int stack[128], sp = 0, cur = 0, done = 0;
       while (!done) {
-        if (cc == 0) {
-          const DNode* nd = &nodes[ci];
+        if ((cur & 31) == 0) {
+          const DNode* nd = &nodes[cur >> 5];
           nv += 1;
-          const float lo0[3] = {nd->b0[0], nd->b0[2], nd->b2[0]}, hi0[3] = {nd->b0[1], nd->b0[3], nd->b2[1]};
-          const float lo1[3] = {nd->b1[0], nd->b1[2], nd->b2[2]}, hi1[3] = {nd->b1[1], nd->b1[3], nd->b2[3]};
-          float l[3], h[3];
-          const float o[3] = {r.org.x, r.org.y, r.org.z}, iv[3] = {inv.x, inv.y, inv.z};
-          for (int k = 0; k < 3; ++k) { l[k] = (lo0[k] - o[k]) * iv[k]; h[k] = (hi0[k] - o[k]) * iv[k]; }
-          const float n0 = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
-          const float f0 = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
-          for (int k = 0; k < 3; ++k) { l[k] = (lo1[k] - o[k]) * iv[k]; h[k] = (hi1[k] - o[k]) * iv[k]; }
-          const float n1 = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
-          const float f1 = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
-          const int h0 = n0 <= f0 * 1.00000036f, h1 = n1 <= f1 * 1.00000036f;
-          if (h0 && h1) {
-            const int sw = n1 < n0;
-            const int nI = sw ? nd->c[1] : nd->c[0], nC = sw ? nd->c[3] : nd->c[2];
-            const int fI = sw ? nd->c[0] : nd->c[1], fC = sw ? nd->c[2] : nd->c[3];
-            stack[sp++] = (fI << 5) | fC;
-            ci = nI; cc = nC;
-            continue;
-          } else if (h0 || h1) {
-            ci = h0 ? nd->c[0] : nd->c[1];
-            cc = h0 ? nd->c[2] : nd->c[3];
+          float t[4];
+          int c[4];
+          for (int k = 0; k < 4; ++k) {
+            const float lo[3] = {nd->lox[k], nd->loy[k], nd->loz[k]}, hi[3] = {nd->hix[k], nd->hiy[k], nd->hiz[k]};
+            float l[3], h[3];
+            for (int a = 0; a < 3; ++a) { l[a] = (lo[a] - o[a]) * iv[a]; h[a] = (hi[a] - o[a]) * iv[a]; }
+            const float nn = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
+            const float ff = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
+            const int hit = nn <= ff * 1.00000036f && nd->child[k] != -1;
+            t[k] = hit ? nn : INF;
+            c[k] = nd->child[k];
+          }
+          /* 5-comparator sort network, as the kernel's sort4 */
+          static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+          for (int m = 0; m < 5; ++m) {
+            const int a = net[m][0], b = net[m][1];
+            if (t[b] < t[a]) {
+              const float tt = t[a]; t[a] = t[b]; t[b] = tt;
+              const int cc = c[a]; c[a] = c[b]; c[b] = cc;
+            }
+          }
+          if (t[3] < INF) stack[sp++] = c[3];
+          if (t[2] < INF) stack[sp++] = c[2];
+          if (t[1] < INF) stack[sp++] = c[1];
+          if (t[0] < INF) {
+            cur = c[0];
             continue;
           }
         } else {
+          const int ci = cur >> 5, cc = cur & 31;
           for (int k = 0; k < cc; ++k) {
             const DTri* t = &tris[ci + k];
             tv += 1;
@@ -2015,9 +2027,7 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
           if (done) break;
         }
         if (sp == 0) break;
-        const int e = stack[--sp];
-        ci = e >> 5;
-        cc = e & 31;
+        cur = stack[--sp];
       }
     }
     if (hit4) {

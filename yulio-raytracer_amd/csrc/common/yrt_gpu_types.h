@@ -3,9 +3,11 @@
 // Everything the kernels read is a flat array uploaded once per rtCommit(scene)
 // (the reference rebuilt the Embree BVH at every commit, api/scene_flat.h:72-97).
 //
-//  BVH (binary, SAH, built on the host — device/bvh_build.cpp):
-//    GpuNode   64 B  both children's AABBs + (child, count) pairs, Aila-Laine style so
-//                    one 64-B line serves the two box tests of a traversal step.
+//  BVH (4-wide, collapsed from a binned-SAH BVH2 built on the host — device/bvh_build.cpp):
+//    GpuNode  128 B  the four children's AABBs as planes [axis lo/hi][child] (so a packed
+//                    op tests two children's planes at once) + four child references
+//                    (index << 5 | count: count 0 = inner node, 1..31 = leaf triangle
+//                    range, -1 = empty slot).
 //    GpuTri    48 B  Embree-convention Moeller-Trumbore triangle in leaf order:
 //                    v0, e1 = v0-v1, e2 = v2-v0 (rtcore triangle convention);
 //                    v0.w = global triangle id (int bits), e1.w = flags (cull bit).
@@ -24,12 +26,11 @@ enum GeomKind : int32_t { GEOM_MESH_FULL = 0, GEOM_MESH_NORMALS = 1, GEOM_TRIANG
 enum GeomFlags : int32_t { GF_NORMALS = 1, GF_TEXCOORDS = 2, GF_CULL = 4 };
 
 struct GpuNode {
-  float b0[4];  // c0.lo.x c0.hi.x c0.lo.y c0.hi.y
-  float b1[4];  // c1.lo.x c1.hi.x c1.lo.y c1.hi.y
-  float b2[4];  // c0.lo.z c0.hi.z c1.lo.z c1.hi.z
-  int32_t c[4]; // child0, child1, count0, count1 (count 0: inner node index; >0: leaf tri range)
+  float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];  // per child
+  int32_t child[4];  // (index << 5) | count ; -1 = empty
+  int32_t pad[4];
 };
-static_assert(sizeof(GpuNode) == 64, "node is one 64-B line");
+static_assert(sizeof(GpuNode) == 128, "node is one 128-B line");
 
 struct GpuTri {
   float v0[4];  // xyz, w = global triangle id (bits)

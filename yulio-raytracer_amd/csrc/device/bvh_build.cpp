@@ -1,10 +1,12 @@
-// bvh_build.cpp — host binned-SAH BVH2 builder for the GPU traversal kernels.
+// bvh_build.cpp — host BVH builder for the GPU traversal kernels.
 //
 // Replaces Embree's rtcCommit SAH build (api/scene_flat.h:72-97).
-// Output is the flat 64-B node / 48-B triangle layout of common/yrt_gpu_types.h.
+// A binned-SAH BVH2 is built first and then collapsed into the 4-wide 128-B node /
+// 48-B triangle layout of common/yrt_gpu_types.h: each 4-wide node takes a BVH2 node's
+// two children and repeatedly opens its largest-area inner child until it has four.
 // Guarantees the traversal kernel's invariants: root is an inner node, leaves hold 1..31
-// triangles, and no inner node is deeper than YRT_STACK_DEPTH-1 (forced object-median
-// splits below a depth chosen from log2(N)), so the per-lane LDS stack never overflows.
+// triangles, and the worst-case traversal stack (3 pushes per 4-wide level) stays below
+// YRT_STACK_DEPTH (forced object-median splits below a depth chosen from log2(N)).
 #include "bvh_build.h"
 
 #include <math.h>
@@ -41,9 +43,14 @@ struct Prim {
   int id;
 };
 
+struct Node2 {
+  Box b[2];
+  int idx[2], cnt[2];  // cnt 0: inner BVH2 node idx; > 0: leaf range [idx, idx+cnt)
+};
+
 struct Builder {
   std::vector<Prim> prims;
-  std::vector<GpuNode> nodes;
+  std::vector<Node2> nodes;
   int maxLeaf = 8;
   int medianDepth = 24;
   int maxDepthSeen = 0;
@@ -147,11 +154,59 @@ struct Builder {
     Box b0, b1;
     child(b, m, depth + 1, i0, c0, b0);
     child(m, e, depth + 1, i1, c1, b1);
-    GpuNode& n = nodes[ni];
-    n.b0[0] = b0.lo[0]; n.b0[1] = b0.hi[0]; n.b0[2] = b0.lo[1]; n.b0[3] = b0.hi[1];
-    n.b1[0] = b1.lo[0]; n.b1[1] = b1.hi[0]; n.b1[2] = b1.lo[1]; n.b1[3] = b1.hi[1];
-    n.b2[0] = b0.lo[2]; n.b2[1] = b0.hi[2]; n.b2[2] = b1.lo[2]; n.b2[3] = b1.hi[2];
-    n.c[0] = i0; n.c[1] = i1; n.c[2] = c0; n.c[3] = c1;
+    Node2& n = nodes[ni];
+    n.b[0] = b0;
+    n.b[1] = b1;
+    n.idx[0] = i0; n.idx[1] = i1;
+    n.cnt[0] = c0; n.cnt[1] = c1;
+    return ni;
+  }
+};
+
+struct Ref {
+  Box b;
+  int idx, cnt;
+};
+
+struct Collapser {
+  const std::vector<Node2>& in;
+  std::vector<GpuNode> out;
+  int maxStack = 0;  // worst-case traversal stack: sum over a root path of (children - 1)
+  explicit Collapser(const std::vector<Node2>& n) : in(n) {}
+
+  // Emits the 4-wide node for BVH2 inner node `n2`; returns its index.
+  int collapse(int n2, int stackAbove) {
+    Ref ch[4];
+    int k = 2;
+    for (int j = 0; j < 2; ++j) ch[j] = Ref{in[n2].b[j], in[n2].idx[j], in[n2].cnt[j]};
+    while (k < 4) {
+      int best = -1;
+      float bestArea = -1.f;
+      for (int j = 0; j < k; ++j)
+        if (ch[j].cnt == 0 && ch[j].b.area() > bestArea) { bestArea = ch[j].b.area(); best = j; }
+      if (best < 0) break;
+      const Node2& o = in[ch[best].idx];
+      ch[best] = Ref{o.b[0], o.idx[0], o.cnt[0]};
+      ch[k++] = Ref{o.b[1], o.idx[1], o.cnt[1]};
+    }
+    const int ni = (int)out.size();
+    out.emplace_back();
+    const int stackHere = stackAbove + (k - 1);
+    if (stackHere > maxStack) maxStack = stackHere;
+    int refs[4] = {-1, -1, -1, -1};
+    for (int j = 0; j < k; ++j) {
+      if (ch[j].cnt == 0) refs[j] = collapse(ch[j].idx, stackHere) << 5;
+      else refs[j] = (ch[j].idx << 5) | ch[j].cnt;
+    }
+    GpuNode& g = out[ni];
+    memset(&g, 0, sizeof(g));
+    for (int j = 0; j < 4; ++j) {
+      const bool v = j < k;
+      g.lox[j] = v ? ch[j].b.lo[0] : 0.f; g.hix[j] = v ? ch[j].b.hi[0] : 0.f;
+      g.loy[j] = v ? ch[j].b.lo[1] : 0.f; g.hiy[j] = v ? ch[j].b.hi[1] : 0.f;
+      g.loz[j] = v ? ch[j].b.lo[2] : 0.f; g.hiz[j] = v ? ch[j].b.hi[2] : 0.f;
+      g.child[j] = refs[j];
+    }
     return ni;
   }
 };
@@ -174,15 +229,14 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
     for (int k = 0; k < 3; ++k) p.c[k] = 0.5f * (p.b.lo[k] + p.b.hi[k]);
     p.id = i;
   }
+  // A BVH2 path of depth D collapses to about D/2 four-wide levels of <= 3 pushes each.
   const int levels = (int)ceil(log2(std::max(1.0, N / 16.0)));
-  B.medianDepth = std::max(0, std::min(28, (stackDepth - 2) - levels));
+  B.medianDepth = std::max(0, std::min(28, (2 * stackDepth) / 3 - 2 - levels));
   if (N == 1) {
-    GpuNode n;
-    Box b = B.prims[0].b;
-    n.b0[0] = n.b1[0] = b.lo[0]; n.b0[1] = n.b1[1] = b.hi[0];
-    n.b0[2] = n.b1[2] = b.lo[1]; n.b0[3] = n.b1[3] = b.hi[1];
-    n.b2[0] = n.b2[2] = b.lo[2]; n.b2[1] = n.b2[3] = b.hi[2];
-    n.c[0] = n.c[1] = 0; n.c[2] = n.c[3] = 1;
+    Node2 n;
+    n.b[0] = n.b[1] = B.prims[0].b;
+    n.idx[0] = 0; n.cnt[0] = 1;
+    n.idx[1] = 0; n.cnt[1] = 1;
     B.nodes.push_back(n);
   } else {
     bool leaf = false;
@@ -190,10 +244,12 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
     if (leaf || m <= 0 || m >= N) m = N / 2;
     B.inner(0, m, N, 0);
   }
-  out.maxDepth = B.maxDepthSeen;
-  if (out.maxDepth > stackDepth - 1)
-    throw std::runtime_error("BVH deeper than the traversal stack; raise YRT_STACK_DEPTH");
-  out.nodes = std::move(B.nodes);
+  Collapser C(B.nodes);
+  C.collapse(0, 0);
+  out.maxDepth = C.maxStack;
+  if (C.maxStack > stackDepth - 1)
+    throw std::runtime_error("BVH traversal stack bound exceeds YRT_STACK_DEPTH");
+  out.nodes = std::move(C.out);
   out.order.resize(N);
   out.tris.resize(N);
   for (int i = 0; i < N; ++i) {

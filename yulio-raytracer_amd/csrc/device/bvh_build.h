@@ -1,4 +1,4 @@
-// bvh_build.h — host BVH2 builder (see bvh_build.cpp).
+// bvh_build.h — host 4-wide BVH builder (see bvh_build.cpp).
 #pragma once
 
 #include <stdint.h>
@@ -13,7 +13,7 @@ struct BvhResult {
   std::vector<GpuNode> nodes;
   std::vector<GpuTri> tris;   // leaf order
   std::vector<int> order;     // leaf slot -> global triangle id
-  int maxDepth = 0;
+  int maxDepth = 0;           // worst-case traversal stack entries (scene info 'bvhDepth')
 };
 
 // v: 9 floats (v0,v1,v2) per global triangle id; flags: per-triangle GpuTri flags (bit0 cull)

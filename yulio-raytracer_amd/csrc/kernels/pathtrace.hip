@@ -270,8 +270,12 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 #ifndef YRT_REFILL
 #define YRT_REFILL 16
 #endif
+#ifndef YRT_TRACE_WAVES
+#define YRT_TRACE_WAVES 6
+#endif
 template <bool ANY>
-__global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const float4* __restrict__ org,
+__global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_TRACE_WAVES))) void k_trace(
+    SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
@@ -324,9 +328,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
       curCnt = e_ & 31;                                                           \
     }                                                                             \
   } while (0)
-  RayPre r;
-  r.org = r.dir = r.inv = v3s(0.f);
-  r.tnear = r.tfar = 0.f;
+  // ray kept as plain vectors across iterations (a loop-carried RayPre struct ends up in
+  // scratch: the vectorizer's straddling loads defeat SROA); rebuilt in registers per step
+  float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, ri = ro;
   Hit best;
   best.t = best.u = best.v = 0.f;
   best.tri = -1;
@@ -341,13 +345,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
           const unsigned li = next + (unsigned)__popcll(idle & ltMask);
           if (li < end) {
             q = qmap_phys(qm, segCap, li);
-            const float4 o = org[q], d = dir[q];
-            r.org = v3(o.x, o.y, o.z);
-            r.dir = v3(d.x, d.y, d.z);
-            r.inv = v3(safe_inv(d.x), safe_inv(d.y), safe_inv(d.z));
-            r.tnear = o.w;
-            r.tfar = d.w;
-            best.t = r.tfar;
+            ro = org[q];
+            rd = dir[q];
+            ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
+            best.t = rd.w;
             best.u = best.v = 0.f;
             best.tri = -1;
             sp = 0;
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
             curCnt = 0;
             pendCnt = 0;
             // NaN tfar (tMaxShadowRay = inf): no hit, nothing to traverse
-            has = r.tfar >= r.tnear;
+            has = rd.w >= ro.w;
             if (!has) {
               if (ANY) occOut[q] = 0;
               else hitOut[q] = make_float4(best.t, 0.f, 0.f, __int_as_float(-1));
@@ -368,25 +369,30 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_trace(SceneView sv, const f
       }
     }
     if (!has) continue;
+    RayPre r;
+    r.org = v3(ro.x, ro.y, ro.z);
+    r.dir = v3(rd.x, rd.y, rd.z);
+    r.inv = v3(ri.x, ri.y, ri.z);
+    r.tnear = ro.w;
+    r.tfar = rd.w;
 
     // ---- inner-node phase ("while-while" with speculative leaf postponing, Aila & Laine
     // 2009): a lane that reaches a leaf parks it in pend* and keeps descending; the phase
     // ends when every traversing lane holds a parked leaf or no lane is at an inner node.
     while (true) {
       if (curCnt == 0) {
-        const GpuNode nd = nodes[curIdx];
-        bool h0, h1;
-        float t0, t1;
-        box2(nd, r, best.t, h0, h1, t0, t1);
-        // branch-light child selection: first = nearer hit child (or the only one)
-        const bool both = h0 && h1;
-        const bool swap = both ? (t1 < t0) : !h0;
-        const int fI = swap ? nd.c[1] : nd.c[0], fC = swap ? nd.c[3] : nd.c[2];
-        const int sI = swap ? nd.c[0] : nd.c[1], sC = swap ? nd.c[2] : nd.c[3];
-        if (both) YRT_PUSH((sI << 5) | sC);
-        if (h0 || h1) {
-          curIdx = fI;
-          curCnt = fC;
+        float t[4];
+        int c[4];
+        box4(nodes + curIdx, r, best.t, t, c);
+        sort4(t, c);
+        // nearest hit child next; the other hits pushed farthest-first
+        const float INF = __int_as_float(0x7f800000);
+        if (t[3] < INF) YRT_PUSH(c[3]);
+        if (t[2] < INF) YRT_PUSH(c[2]);
+        if (t[1] < INF) YRT_PUSH(c[1]);
+        if (t[0] < INF) {
+          curIdx = c[0] >> 5;
+          curCnt = c[0] & 31;
         } else {
           YRT_POP();
         }

@@ -22,7 +22,7 @@
 #include "../common/yrt_math.h"
 
 #ifndef YRT_STACK_DEPTH
-#define YRT_STACK_DEPTH 64   // bound on BVH depth + 1 (device/bvh_build.cpp enforces it)
+#define YRT_STACK_DEPTH 64   // bound on traversal stack entries + 1 (device/bvh_build.cpp enforces it)
 #endif
 #ifndef YRT_LDS_STACK
 #define YRT_LDS_STACK 16     // top entries kept in LDS; deeper ones spill (power of two)
@@ -50,23 +50,55 @@ struct RayPre {
   float tnear, tfar;
 };
 
-__device__ __forceinline__ void box2(const GpuNode& n, const RayPre& r, float tmax, bool& h0, bool& h1,
-                                     float& t0, float& t1) {
-  // child 0
-  float lx0 = (n.b0[0] - r.org.x) * r.inv.x, hx0 = (n.b0[1] - r.org.x) * r.inv.x;
-  float ly0 = (n.b0[2] - r.org.y) * r.inv.y, hy0 = (n.b0[3] - r.org.y) * r.inv.y;
-  float lz0 = (n.b2[0] - r.org.z) * r.inv.z, hz0 = (n.b2[1] - r.org.z) * r.inv.z;
-  float lx1 = (n.b1[0] - r.org.x) * r.inv.x, hx1 = (n.b1[1] - r.org.x) * r.inv.x;
-  float ly1 = (n.b1[2] - r.org.y) * r.inv.y, hy1 = (n.b1[3] - r.org.y) * r.inv.y;
-  float lz1 = (n.b2[2] - r.org.z) * r.inv.z, hz1 = (n.b2[3] - r.org.z) * r.inv.z;
-  float n0 = fmaxf(fmaxf(fminf(lx0, hx0), fminf(ly0, hy0)), fmaxf(fminf(lz0, hz0), r.tnear));
-  float f0 = fminf(fminf(fmaxf(lx0, hx0), fmaxf(ly0, hy0)), fminf(fmaxf(lz0, hz0), tmax));
-  float n1 = fmaxf(fmaxf(fminf(lx1, hx1), fminf(ly1, hy1)), fmaxf(fminf(lz1, hz1), r.tnear));
-  float f1 = fminf(fminf(fmaxf(lx1, hx1), fmaxf(ly1, hy1)), fminf(fmaxf(lz1, hz1), tmax));
-  h0 = n0 <= f0 * YRT_BOX_ROBUST;
-  h1 = n1 <= f1 * YRT_BOX_ROBUST;
-  t0 = n0;
-  t1 = n1;
+// Entry distances of the four children of a 4-wide node (INFINITY = missed / empty slot).
+// Slab distances (b - o) * inv are computed two children at a time with packed ops
+// (v_pk_add_f32 / v_pk_mul_f32); the robust factor widens the exit distance as before.
+__device__ __forceinline__ void box4(const GpuNode* __restrict__ np, const RayPre& r, float tmax, float t[4],
+                                     int c[4]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const float4* q = (const float4*)np;
+  const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+  const int4 ch = *(const int4*)(q + 6);
+  const f2 ox = {r.org.x, r.org.x}, oy = {r.org.y, r.org.y}, oz = {r.org.z, r.org.z};
+  const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
+  const f2 lx01 = (f2{lx.x, lx.y} - ox) * ix, lx23 = (f2{lx.z, lx.w} - ox) * ix;
+  const f2 hx01 = (f2{hx.x, hx.y} - ox) * ix, hx23 = (f2{hx.z, hx.w} - ox) * ix;
+  const f2 ly01 = (f2{ly.x, ly.y} - oy) * iy, ly23 = (f2{ly.z, ly.w} - oy) * iy;
+  const f2 hy01 = (f2{hy.x, hy.y} - oy) * iy, hy23 = (f2{hy.z, hy.w} - oy) * iy;
+  const f2 lz01 = (f2{lz.x, lz.y} - oz) * iz, lz23 = (f2{lz.z, lz.w} - oz) * iz;
+  const f2 hz01 = (f2{hz.x, hz.y} - oz) * iz, hz23 = (f2{hz.z, hz.w} - oz) * iz;
+  const float INF = __int_as_float(0x7f800000);
+#define YRT_CHILD(k, LX, HX, LY, HY, LZ, HZ, CH)                                                          \
+  do {                                                                                                    \
+    const float nn = fmaxf(fmaxf(fminf(LX, HX), fminf(LY, HY)), fmaxf(fminf(LZ, HZ), r.tnear));          \
+    const float ff = fminf(fminf(fmaxf(LX, HX), fmaxf(LY, HY)), fminf(fmaxf(LZ, HZ), tmax));             \
+    t[k] = ((nn <= ff * YRT_BOX_ROBUST) && (CH) != -1) ? nn : INF;                                        \
+    c[k] = (CH);                                                                                          \
+  } while (0)
+  YRT_CHILD(0, lx01.x, hx01.x, ly01.x, hy01.x, lz01.x, hz01.x, ch.x);
+  YRT_CHILD(1, lx01.y, hx01.y, ly01.y, hy01.y, lz01.y, hz01.y, ch.y);
+  YRT_CHILD(2, lx23.x, hx23.x, ly23.x, hy23.x, lz23.x, hz23.x, ch.z);
+  YRT_CHILD(3, lx23.y, hx23.y, ly23.y, hy23.y, lz23.y, hz23.y, ch.w);
+#undef YRT_CHILD
+}
+
+// Sorts the four (t, child) pairs by t ascending (5-comparator network, stable for equal t).
+__device__ __forceinline__ void sort4(float t[4], int c[4]) {
+#define YRT_CSWAP(a, b)                          \
+  do {                                           \
+    const bool sw = t[b] < t[a];                 \
+    const float ta = sw ? t[b] : t[a];           \
+    const float tb = sw ? t[a] : t[b];           \
+    const int ca = sw ? c[b] : c[a];             \
+    const int cb = sw ? c[a] : c[b];             \
+    t[a] = ta; t[b] = tb; c[a] = ca; c[b] = cb;  \
+  } while (0)
+  YRT_CSWAP(0, 1);
+  YRT_CSWAP(2, 3);
+  YRT_CSWAP(0, 2);
+  YRT_CSWAP(1, 3);
+  YRT_CSWAP(1, 2);
+#undef YRT_CSWAP
 }
 
 // One triangle; returns true and t when the ray hits within (tnear, tfar). U, V, absDen are
@@ -96,44 +128,39 @@ __device__ __forceinline__ bool tri_test_t(const GpuTri& tr, const RayPre& r, fl
   return ok;
 }
 
+// Plain depth-first traversal (rtPick, DebugRenderer): nearest child first, the other hit
+// children pushed farthest-first; same closest-hit rule as the wavefront kernel.
 template <bool ANY>
 __device__ __forceinline__ Hit traverse(const GpuNode* __restrict__ nodes, const GpuTri* __restrict__ tris,
-                                        const RayPre& r, int* __restrict__ stack /* LDS, this lane's column */) {
+                                        const RayPre& r, int* __restrict__ stack /* LDS, unused */) {
+  (void)stack;
   Hit best;
   best.t = r.tfar;
   best.u = best.v = 0.0f;
   best.tri = -1;
   // NaN tfar (tMaxShadowRay = inf): every comparison is false, no hit.
   if (!(r.tfar >= r.tnear)) return best;
+  int pst[YRT_STACK_DEPTH];
   int sp = 0;
-  int spill[YRT_STACK_DEPTH > YRT_LDS_STACK ? YRT_STACK_DEPTH - YRT_LDS_STACK : 1];
-  // stack entry: (index << 5) | count — count 0 => inner node, 1..31 => leaf range
-  int curIdx = 0, curCnt = 0;
+  int cur = 0;  // (index << 5) | count
   while (true) {
-    if (curCnt == 0) {
-      const GpuNode n = nodes[curIdx];
-      bool h0, h1;
-      float t0, t1;
-      box2(n, r, best.t, h0, h1, t0, t1);
-      if (h0 && h1) {
-        bool swap = t1 < t0;
-        int nearI = swap ? n.c[1] : n.c[0], nearC = swap ? n.c[3] : n.c[2];
-        int farI = swap ? n.c[0] : n.c[1], farC = swap ? n.c[2] : n.c[3];
-        const int e = (farI << 5) | farC;
-        if (sp < YRT_LDS_STACK) stack[sp * YRT_TRACE_BLOCK] = e;
-        else spill[sp - YRT_LDS_STACK] = e;
-        sp += 1;
-        curIdx = nearI;
-        curCnt = nearC;
-        continue;
-      } else if (h0 || h1) {
-        curIdx = h0 ? n.c[0] : n.c[1];
-        curCnt = h0 ? n.c[2] : n.c[3];
+    if ((cur & 31) == 0) {
+      float t[4];
+      int c[4];
+      box4(nodes + (cur >> 5), r, best.t, t, c);
+      sort4(t, c);
+      const float INF = __int_as_float(0x7f800000);
+      if (t[3] < INF) pst[sp++] = c[3];
+      if (t[2] < INF) pst[sp++] = c[2];
+      if (t[1] < INF) pst[sp++] = c[1];
+      if (t[0] < INF) {
+        cur = c[0];
         continue;
       }
     } else {
-      for (int i = 0; i < curCnt; ++i) {
-        const GpuTri tr = tris[curIdx + i];
+      const int idx = cur >> 5, cnt = cur & 31;
+      for (int i = 0; i < cnt; ++i) {
+        const GpuTri tr = tris[idx + i];
         float t, U, V, absDen;
         bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
         int gid = __float_as_int(tr.v0[3]);
@@ -156,10 +183,7 @@ __device__ __forceinline__ Hit traverse(const GpuNode* __restrict__ nodes, const
       }
     }
     if (sp == 0) break;
-    sp -= 1;
-    const int e = sp < YRT_LDS_STACK ? stack[sp * YRT_TRACE_BLOCK] : spill[sp - YRT_LDS_STACK];
-    curIdx = e >> 5;
-    curCnt = e & 31;
+    cur = pst[--sp];
   }
   return best;
 }
