@@ -177,6 +177,10 @@ YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
 YRT_API int yrtSetRayCapture(YRTDevice dev, int maxPerDepth);
 YRT_API int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* org4, float* dir4, size_t maxRays,
                                    double* totalInBatch);
+/* Profiling builds (-DYRT_PROFILE) only: k_trace SIMD-utilization counters since the last
+ * reset (outer iterations, lanes with a ray, node-phase iterations, lanes at a node, leaf
+ * passes, triangle-loop iterations, useful triangle tests, 0). Returns -1 otherwise. */
+YRT_API int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset);
 /* Decoder check: 8-bit pixels of a .jpg/.png in file row order (top row first), before the
  * Image4c flip/requantization of rtNewImageFromFile. Call with out=NULL to get the size. */
 YRT_API int yrtDebugDecodeImage(const char* file, int* width, int* height, int* channels, uint8_t* out,

@@ -51,7 +51,10 @@ struct Node2 {
 struct Builder {
   std::vector<Prim> prims;
   std::vector<Node2> nodes;
-  int maxLeaf = 8;
+#ifndef YRT_MAX_LEAF
+#define YRT_MAX_LEAF 8
+#endif
+  int maxLeaf = YRT_MAX_LEAF;
   int medianDepth = 24;
   int maxDepthSeen = 0;
 

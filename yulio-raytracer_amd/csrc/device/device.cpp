@@ -1156,6 +1156,13 @@ int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* org4, fl
   DEV_END(-1)
 }
 
+int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset) {
+  DEV_GUARD(dev, -1)
+  HIP_CHECK(hipDeviceSynchronize());
+  return trace_profile((unsigned long long*)out8, reset);
+  DEV_END(-1)
+}
+
 int yrtSetTileShard(YRTDevice dev, int index, int count) {
   DEV_GUARD(dev, -1)
   if (count < 1 || index < 0 || index >= count) throw std::runtime_error("invalid shard");

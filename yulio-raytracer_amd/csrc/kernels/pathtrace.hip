@@ -270,6 +270,18 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 #ifndef YRT_REFILL
 #define YRT_REFILL 16
 #endif
+#ifdef YRT_PROFILE
+// [0] outer iterations x waves, [1] lanes holding a ray at outer iterations,
+// [2] node-phase iterations, [3] lanes visiting a node, [4] leaf passes with work,
+// [5] triangle-loop iterations (max leaf size per pass), [6] useful triangle tests
+__device__ unsigned long long g_traceProfile[8];
+#define YRT_PROF(i, v) prof[i] += (unsigned long long)(v)
+#else
+#define YRT_PROF(i, v) ((void)0)
+#endif
+#ifndef YRT_NODE_BIAS
+#define YRT_NODE_BIAS 4  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
+#endif
 #ifndef YRT_TRACE_WAVES
 #define YRT_TRACE_WAVES 6
 #endif
@@ -336,9 +348,20 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   best.tri = -1;
   const unsigned long long ltMask = (1ull << lane) - 1ull;
 
+#ifdef YRT_PROFILE
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   while (true) {
+    // retire lanes whose traversal is complete
+    if (has && curCnt < 0 && pendCnt == 0) {
+      if (ANY) occOut[q] = 0;
+      else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
+      has = false;
+    }
     const unsigned long long idle = __ballot(!has);
     const int nIdle = __popcll(idle);
+    YRT_PROF(0, 1);
+    YRT_PROF(1, 64 - nIdle);
     if (nIdle >= YRT_REFILL) {
       if (next < end) {
         if (!has) {
@@ -365,10 +388,13 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         }
         next += (unsigned)nIdle;
       } else if (nIdle == 64) {
+#ifdef YRT_PROFILE
+        if (lane == 0)
+          for (int k = 0; k < 8; ++k) atomicAdd(&g_traceProfile[k], prof[k]);
+#endif
         break;
       }
     }
-    if (!has) continue;
     RayPre r;
     r.org = v3(ro.x, ro.y, ro.z);
     r.dir = v3(rd.x, rd.y, rd.z);
@@ -376,11 +402,19 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     r.tnear = ro.w;
     r.tfar = rd.w;
 
-    // ---- inner-node phase ("while-while" with speculative leaf postponing, Aila & Laine
-    // 2009): a lane that reaches a leaf parks it in pend* and keeps descending; the phase
-    // ends when every traversing lane holds a parked leaf or no lane is at an inner node.
-    while (true) {
-      if (curCnt == 0) {
+    // One step per iteration, chosen wave-uniformly ("while-while" with speculative leaf
+    // parking, Aila & Laine 2009): node steps while any lane still searches for its first
+    // leaf (a lane reaching a leaf parks it and keeps descending), then one leaf step in
+    // which every lane tests one leaf. Refill above runs every iteration, so lanes that
+    // finish rejoin at once instead of idling until the wave's phase ends.
+    // node step when more lanes can descend than are blocked on a leaf (cur is a leaf while
+    // another is parked, or only a parked leaf is left); otherwise a leaf step
+    const int nNode = __popcll(__ballot(has && curCnt == 0));
+    const int nBlocked = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
+    if (nNode * 4 > nBlocked * YRT_NODE_BIAS) {
+      YRT_PROF(2, 1);
+      YRT_PROF(3, __popcll(__ballot(has && curCnt == 0)));
+      if (has && curCnt == 0) {
         float t[4];
         int c[4];
         box4(nodes + curIdx, r, best.t, t, c);
@@ -402,19 +436,23 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
       }
-      if (!__any(curCnt == 0)) break;
-      if (!__any(curCnt == 0 && pendCnt == 0)) break;
-    }
-
-    // ---- leaf phase: the parked leaf, then the current entry if it is a leaf too
-    bool found = false;
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-      int lIdx = pendIdx, lCnt = pendCnt;
-      if (pass == 1) {
-        lIdx = curIdx;
-        lCnt = curCnt > 0 ? curCnt : 0;
+    } else {
+      // leaf step: the parked leaf, or else the current entry when it is a leaf
+      const bool usePend = pendCnt > 0;
+      const int lIdx = usePend ? pendIdx : curIdx;
+      const int lCnt = !has ? 0 : usePend ? pendCnt : (curCnt > 0 ? curCnt : 0);
+#ifdef YRT_PROFILE
+      {
+        int mx = lCnt;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        int sm = lCnt;
+        for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+        YRT_PROF(4, mx > 0 ? 1 : 0);
+        YRT_PROF(5, mx);
+        YRT_PROF(6, sm);
       }
+#endif
+      bool found = false;
       for (int i = 0; i < lCnt && !found; ++i) {
         const GpuTri tr = tris[lIdx + i];
         float t, U, V, absDen;
@@ -433,16 +471,14 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           }
         }
       }
-      if (pass == 0) pendCnt = 0;
-      else if (curCnt > 0) YRT_POP();
-    }
-    if (ANY && found) {
-      occOut[q] = 1;
-      has = false;
-    } else if (curCnt < 0) {
-      if (ANY) occOut[q] = 0;
-      else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
-      has = false;
+      if (lCnt > 0) {
+        if (usePend) pendCnt = 0;
+        else YRT_POP();
+      }
+      if (ANY && found) {
+        occOut[q] = 1;
+        has = false;
+      }
     }
   }
 }
@@ -1086,6 +1122,21 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_pick(SceneView sv, const Gp
   const Hit h = traverse<false>(sv.nodes, sv.tris, r, stack + threadIdx.x);
   const V3 p = org + h.t * dir;
   out[0] = make_float4(p.x, p.y, p.z, __int_as_float(h.tri));
+}
+
+int trace_profile(unsigned long long* out8, int reset) {
+#ifdef YRT_PROFILE
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_traceProfile), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_traceProfile), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+#else
+  (void)out8;
+  (void)reset;
+  return -1;
+#endif
 }
 
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s) {

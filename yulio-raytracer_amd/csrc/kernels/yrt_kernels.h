@@ -107,6 +107,8 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
+// YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
+int trace_profile(unsigned long long* out8, int reset);
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);

@@ -144,6 +144,7 @@ _sig(dev, "yrtSetBatchCapacity", i32, vp, C.c_int64)
 _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
 _sig(dev, "yrtSetRayCapture", i32, vp, i32)
 _sig(dev, "yrtGetCapturedRays", C.c_int64, vp, i32, i32, vp, vp, sz, C.POINTER(C.c_double))
+_sig(dev, "yrtDebugTraceProfile", i32, vp, C.POINTER(C.c_uint64), i32)
 _sig(dev, "yrtDebugDecodeImage", i32, cstr, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), vp, sz)
 _sig(dev, "yrtDebugSampleTable", i32, i32, i32, i32, i32, i32, cstr, PF, sz)
 
