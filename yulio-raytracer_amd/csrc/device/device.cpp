@@ -318,7 +318,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
           capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap);
         EvPair e2{};
         if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
-        launch_shade(sv, fv, pb, bi, d, stream);
+        launch_shade(sv, fv, pb, bi, d, G.materialMask, stream);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, stream)); evs.push_back(e2); }
         if (rp.numLights > 0) {
           EvPair e3{};

@@ -198,6 +198,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S;
   }
+  for (const GpuMaterial& m : materials) S->materialMask |= 1u << m.type;
   S->nodes.upload(bvh.nodes);
   S->tris.upload(bvh.tris);
   S->triGeom.upload(triGeom);

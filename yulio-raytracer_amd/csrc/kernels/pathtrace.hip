@@ -279,6 +279,9 @@ __device__ unsigned long long g_traceProfile[8];
 #else
 #define YRT_PROF(i, v) ((void)0)
 #endif
+#ifndef YRT_TRI_STEP
+#define YRT_TRI_STEP 0
+#endif
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 4  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
@@ -453,7 +456,13 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       }
 #endif
       bool found = false;
-      for (int i = 0; i < lCnt && !found; ++i) {
+#if YRT_TRI_STEP
+      // one triangle per lane per leaf step: no intra-leaf divergence
+      const int lTake = lCnt > 0 ? 1 : 0;
+#else
+      const int lTake = lCnt;
+#endif
+      for (int i = 0; i < lTake && !found; ++i) {
         const GpuTri tr = tris[lIdx + i];
         float t, U, V, absDen;
         bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
@@ -471,10 +480,24 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           }
         }
       }
+#if YRT_TRI_STEP
+      if (lCnt > 0) {
+        if (usePend) {
+          pendIdx += 1;
+          pendCnt -= 1;
+        } else if (curCnt > 1) {
+          curIdx += 1;
+          curCnt -= 1;
+        } else {
+          YRT_POP();
+        }
+      }
+#else
       if (lCnt > 0) {
         if (usePend) pendCnt = 0;
         else YRT_POP();
       }
+#endif
       if (ANY && found) {
         occOut[q] = 1;
         has = false;
@@ -575,8 +598,10 @@ __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V
 }
 
 // Material::shade for the in-scope materials (materials/*.h). May modify dg.Ns (Obj bump).
+template <unsigned MM>
 __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, DG& dg, BRDFSet& bs) {
   bs.n = 0;
+  if (!(MM & mat_bit(m.type))) return;
   switch (m.type) {
     case MAT_MATTE:
       add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
@@ -736,6 +761,7 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
 #ifndef YRT_SHADE_WAVES
 #define YRT_SHADE_WAVES 3
 #endif
+template <unsigned MM>
 __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
   const GpuRenderParams& rp = *fv.rp;
@@ -804,7 +830,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
           dg.Ng = -dg.Ng;
           dg.Ns = -dg.Ns;
         }
-        if (dg.material >= 0) shade_material(sv, sv.materials[dg.material], dg, bs);
+        if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg, bs);
         if (!ignoreVL && dg.light >= 0 && !backfacing) {
           const GpuLight& al = sv.lights[dg.light];
           L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
@@ -836,7 +862,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
             Ls = light_sample(lt, dg, sx, sy, wi, pdf);
           }
           if (!(Ls == v3s(0.f) || pdf == 0.f)) {
-            const V3 brdf = set_eval(bs, wo, dg, wi, BT_DIFFUSE);
+            const V3 brdf = set_eval<comps_of(MM)>(bs, wo, dg, wi, BT_DIFFUSE);
             if (!(brdf == v3s(0.f))) {
               const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
               const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
@@ -880,7 +906,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         const float ss = samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec);
         float pdf;
         uint32_t type;
-        const V3 c = set_sample(bs, wo, dg, sx, sy, ss, nwi, pdf, type);
+        const V3 c = set_sample<comps_of(MM)>(bs, wo, dg, sx, sy, ss, nwi, pdf, type);
         if (!(c == v3s(0.f) || pdf <= 0.f)) {
           nthr = thr * c * rcpf_(pdf);
           const bool nIgnore = (type & BT_DIFFUSE) != 0;
@@ -1088,10 +1114,42 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
                      0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill);
 }
 
+// Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of
+// the scene's materials; YRT_ALL_MATS is the generic fallback.
+static const unsigned kShadeVariants[] = {
+    mat_bit(MAT_UBER),                                                                // Collada (Sponza)
+    mat_bit(MAT_OBJ),                                                                 // OBJ scenes
+    mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT),                                 // cornell spheres
+    mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT),    // test_stereo
+    YRT_ALL_MATS};
+
+template <unsigned MM>
+static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
+                           int depth, hipStream_t s) {
+  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, sv, fv, pb,
+                     bi, depth);
+}
+
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  hipStream_t s) {
-  hipLaunchKernelGGL(k_shade, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, sv, fv, pb, bi,
-                     depth);
+                  unsigned materialMask, hipStream_t s) {
+  unsigned pick = YRT_ALL_MATS;
+  for (unsigned v : kShadeVariants)
+    if ((materialMask & ~v) == 0) {
+      pick = v;
+      break;
+    }
+  switch (pick) {
+    case mat_bit(MAT_UBER): launch_shade_t<mat_bit(MAT_UBER)>(sv, fv, pb, bi, depth, s); break;
+    case mat_bit(MAT_OBJ): launch_shade_t<mat_bit(MAT_OBJ)>(sv, fv, pb, bi, depth, s); break;
+    case mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT):
+      launch_shade_t<mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT)>(sv, fv, pb, bi, depth, s);
+      break;
+    case mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT):
+      launch_shade_t<mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT)>(sv, fv, pb, bi,
+                                                                                                   depth, s);
+      break;
+    default: launch_shade_t<YRT_ALL_MATS>(sv, fv, pb, bi, depth, s); break;
+  }
 }
 
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {

@@ -102,8 +102,10 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
                           int numSegs, int segCap, float4* hit, hipStream_t s);
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s);
+// materialMask: bit MAT_x set for every material type the scene uses (selects a specialized
+// instantiation of the shade kernel)
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  hipStream_t s);
+                  unsigned materialMask, hipStream_t s);
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);

@@ -42,6 +42,20 @@ enum CompKind : int {
   C_SPECULAR = 7,         // Specular(R, exp)                            a=exp
 };
 
+// Material-set specialization: the shade kernel is instantiated for a bitmask of material
+// types (bit MAT_x); only the BRDF components those materials can create are compiled in,
+// which cuts register pressure for scenes with few material types.
+__host__ __device__ constexpr unsigned mat_bit(int m) { return 1u << m; }
+__host__ __device__ constexpr unsigned comp_bit(int c) { return 1u << c; }
+__host__ __device__ constexpr unsigned comps_of(unsigned mats) {
+  return ((mats & (mat_bit(1) | mat_bit(2))) ? comp_bit(0) : 0u) |                                  // Matte(Textured)
+         ((mats & mat_bit(3)) ? (comp_bit(1) | comp_bit(4)) : 0u) |                                 // MetallicPaint
+         ((mats & mat_bit(4)) ? (comp_bit(6) | comp_bit(0) | comp_bit(7)) : 0u) |                   // Obj
+         ((mats & mat_bit(5)) ? (comp_bit(0) | comp_bit(2) | comp_bit(1) | comp_bit(5)) : 0u) |     // Uber
+         ((mats & mat_bit(6)) ? (comp_bit(1) | comp_bit(3)) : 0u);                                  // ThinDielectric
+}
+#define YRT_ALL_MATS 0x7Eu
+
 struct Comp {
   int kind;
   uint32_t type;
@@ -200,7 +214,9 @@ __device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, 
   return c.R * (c.a + 2) * (1.0f / (2.0f * kPi)) * powf(dot(r, wi), c.a) * clampf(dot(wi, dg.Ns));
 }
 
+template <unsigned CM>
 __device__ __forceinline__ V3 comp_eval(const Comp c, V3 wo, const DG& dg, V3 wi) {
+  if (!(CM & comp_bit(c.kind))) return v3s(0.0f);
   switch (c.kind) {
     case C_LAMBERT: return lambert_eval(c.R, dg, wi);
     case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
@@ -211,8 +227,14 @@ __device__ __forceinline__ V3 comp_eval(const Comp c, V3 wo, const DG& dg, V3 wi
 }
 
 // BRDF::sample of one component; returns color, sets wi/pdf.
+template <unsigned CM>
 __device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, float sx, float sy, V3& wi,
                                           float& pdf) {
+  if (!(CM & comp_bit(c.kind))) {
+    pdf = 0.0f;
+    wi = v3s(0.0f);
+    return v3s(0.0f);
+  }
   switch (c.kind) {
     case C_LAMBERT: {
       wi = cosine_hemi(sx, sy, dg.Ns, pdf);
@@ -301,13 +323,14 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, flo
 }
 
 // CompositedBRDF::eval restricted to `type` (compositedbrdf.h:59-65)
+template <unsigned CM>
 __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V3 wi, uint32_t type) {
   V3 c = v3s(0.0f);
 #pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i)
     if (i < bs.n && (bs.c[i].type & type)) {
       const Comp ci = bs.c[i];
-      c = c + comp_eval(ci, wo, dg, wi);
+      c = c + comp_eval<CM>(ci, wo, dg, wi);
     }
   return c;
 }
@@ -316,6 +339,7 @@ __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V
 // (f_i = sum(c_i)/pdf_i over the components that sampled something, normalized by their
 // running sum, CDF with the last entry forced to 1), written with compile-time component
 // indices only so nothing is spilled to scratch.
+template <unsigned CM>
 __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg, float sx, float sy, float ss,
                                          V3& wi_o, float& pdf_o, uint32_t& type_o) {
   float f[YRT_MAX_COMPS];
@@ -335,7 +359,7 @@ __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg,
       V3 wi;
       float pdf = 0.0f;
       const Comp ci = bs.c[i];
-      const V3 c = comp_sample(ci, wo, dg, sx, sy, wi, pdf);
+      const V3 c = comp_sample<CM>(ci, wo, dg, sx, sy, wi, pdf);
       if (!((c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) || pdf <= 0.0f)) {
         ok[i] = true;
         f[i] = (c.x + c.y + c.z) * rcpf_(pdf);
