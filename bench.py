@@ -164,8 +164,19 @@ def main():
         ms, nr, nl = kern[dom]
         bytes_total = nr * per_kind[dom]["bytes_per_ray"]
         achieved = bytes_total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        # HBM bytes per launch of the same kernel from the committed PMC pass on this workload
+        # (tools/gpu_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)
+        traffic = None
+        tf = ROOT / "profiles" / "traffic.json"
+        kname = "k_trace<false>" if dom == "closest" else "k_trace<true>"
+        if tf.exists():
+            try:
+                traffic = round(json.loads(tf.read_text())["kernels"][kname]["hbm_bytes_per_dispatch"])
+            except (KeyError, ValueError):
+                traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": "profiles/traffic.json (rocprofv3 PMC, same workload)" if traffic else None,
                 "kernel": "k_trace_closest" if dom == "closest" else "k_trace_any",
                 "launches": int(nl), "avg_launch_ms": round(ms / max(nl, 1), 4),
                 "algorithmic_bytes_per_launch": round(bytes_total / max(nl, 1)),

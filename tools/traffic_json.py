@@ -22,7 +22,7 @@ def main(root):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
             for k, tag in KERNELS.items():
-                if tag in name:
+                if tag in name or k in name:
                     c = row["Counter_Name"]
                     acc[k][c] += float(row["Counter_Value"])
                     n[k][c].add(row.get("Dispatch_Id", ""))
