@@ -43,6 +43,11 @@ YRT_API void* yrtSessionRender(YRTSession s, int face);
 /* outputMode(-o file): renders and stores the image (.ppm/.pfm/.png; stereo: 12-face strip). */
 YRT_API int yrtSessionOutput(YRTSession s, const char* file);
 
+/* storeImage (common/image/image.cpp:77-104): .jpg (baseline, quality 1..100, the FreeImage
+ * path), .png, .ppm, .pfm. format: 0 RGB8, 1 RGBA8, 2 RGB_FLOAT32, 3 RGBA_FLOAT32; rows top
+ * first, `stride` bytes apart. */
+YRT_API int yrtStoreImage(const char* file, int width, int height, int format, const void* pixels, size_t stride,
+                          int quality);
 /* rt.exe main: parse + output; returns process-style exit code. */
 YRT_API int yrtMain(int argc, const char** argv);
 

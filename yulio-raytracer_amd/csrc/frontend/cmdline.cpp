@@ -7,8 +7,10 @@
 //   outputMode                 :508-905 (mono and non-FPR stereo branches)
 #include <stdio.h>
 #include <string.h>
+#include <dlfcn.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
@@ -372,7 +374,33 @@ static void write_png(const std::string& file, int w, int h, const std::vector<u
   fclose(f);
 }
 
-void store_image(const std::string& file, int w, int h, int fmt, const void* px, size_t stride) {
+// Image3c/Image4c -> Color4 -> byte round trip of the reference's image classes
+// (common/math/color_scalar.h:45-60): byte * one_over_255, then char(clamp(c) * 255): a byte
+// can lose 1 LSB.
+static inline uint8_t requant(uint8_t b) {
+  const float c = b * (1.0f / 255.0f);
+  return (uint8_t)(std::max(0.0f, std::min(c, 1.0f)) * 255.0f);
+}
+
+// 8-bit RGB, top row first, as the reference's storers read it through Image::get.
+static std::vector<uint8_t> to_rgb8(int w, int h, int fmt, const void* px, size_t stride, bool viaColor4) {
+  std::vector<uint8_t> rgb((size_t)w * h * 3);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const uint8_t* row = (const uint8_t*)px + (size_t)y * stride;
+      uint8_t* o = &rgb[((size_t)y * w + x) * 3];
+      if (fmt >= 2) {
+        const float* p = (const float*)row + x * (fmt == 2 ? 3 : 4);
+        for (int k = 0; k < 3; ++k) o[k] = (uint8_t)(std::max(0.0f, std::min(p[k], 1.0f)) * 255.0f);
+      } else {
+        const uint8_t* p = row + x * (fmt == 0 ? 3 : 4);
+        for (int k = 0; k < 3; ++k) o[k] = viaColor4 ? requant(p[k]) : p[k];
+      }
+    }
+  return rgb;
+}
+
+void store_image(const std::string& file, int w, int h, int fmt, const void* px, size_t stride, int quality) {
   const std::string ext = ext_of(file);
   if (ext == "pfm") {
     FILE* f = fopen(file.c_str(), "wb");
@@ -394,19 +422,17 @@ void store_image(const std::string& file, int w, int h, int fmt, const void* px,
     fclose(f);
     return;
   }
-  std::vector<uint8_t> rgb((size_t)w * h * 3);
-  for (int y = 0; y < h; ++y)
-    for (int x = 0; x < w; ++x) {
-      const uint8_t* row = (const uint8_t*)px + (size_t)y * stride;
-      uint8_t* o = &rgb[((size_t)y * w + x) * 3];
-      if (fmt >= 2) {
-        const float* p = (const float*)row + x * (fmt == 2 ? 3 : 4);
-        for (int k = 0; k < 3; ++k) o[k] = (uint8_t)(std::max(0.0f, std::min(p[k], 1.0f)) * 255.0f);
-      } else {
-        const uint8_t* p = row + x * (fmt == 0 ? 3 : 4);
-        o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
-      }
-    }
+  if (ext == "jpg" || ext == "jpeg") {
+    // storeFreeImage (common/image/freeimage.cpp:191-232): 24-bit, (uchar)(clamp(c)*255)
+    const std::vector<uint8_t> rgb = to_rgb8(w, h, fmt, px, stride, true);
+    const std::vector<uint8_t> jpg = encode_jpeg(rgb.data(), w, h, (size_t)w * 3, quality);
+    FILE* f = fopen(file.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot write " + file);
+    fwrite(jpg.data(), 1, jpg.size(), f);
+    fclose(f);
+    return;
+  }
+  const std::vector<uint8_t> rgb = to_rgb8(w, h, fmt, px, stride, false);
   if (ext == "ppm") {
     FILE* f = fopen(file.c_str(), "wb");
     if (!f) throw std::runtime_error("cannot write " + file);
@@ -416,19 +442,73 @@ void store_image(const std::string& file, int w, int h, int fmt, const void* px,
   } else if (ext == "png") {
     write_png(file, w, h, rgb);
   } else {
-    throw std::runtime_error("image format ." + ext + " not supported by this build (JPEG output: SURVEY §8(f) rank 2)");
+    throw std::runtime_error("image format ." + ext + " not supported (use .jpg, .png, .ppm or .pfm)");
   }
 }
 
-// outputMode (renderer.cpp:508-905)
+// Yulio watermark (renderer.cpp:51-97): the 100x100 RGBA resource, loaded through
+// loadFreeImage(data, size, 1, flipVertical, flipHorizontal) into an Image4c.
+static bool load_watermark(std::vector<uint8_t>& rgba, int& w, int& h) {
+  Dl_info info;
+  if (!dladdr((void*)&load_watermark, &info) || !info.dli_fname) return false;
+  std::string dir = path_of(info.dli_fname);
+  const std::string file = dir + "../resources/watermarkwhitetrasp_100x100.png";
+  int c = 0;
+  if (yrtDebugDecodeImage(file.c_str(), &w, &h, &c, nullptr, 0) != 0 || c != 4) return false;
+  std::vector<uint8_t> px((size_t)w * h * 4);
+  if (yrtDebugDecodeImage(file.c_str(), &w, &h, &c, px.data(), px.size()) != 0) return false;
+  // decoded rows are top-first; FreeImage's DIB is bottom-up, so its FlipVertical yields
+  // top-first rows; FlipHorizontal mirrors the columns. Bytes go through b/255.0f and the
+  // Image4c store char(clamp(c)*255).
+  rgba.resize(px.size());
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x)
+      for (int k = 0; k < 4; ++k) {
+        const float f = (float)px[((size_t)y * w + (w - 1 - x)) * 4 + k] / 255.0f;
+        rgba[((size_t)y * w + x) * 4 + k] = (uint8_t)(std::max(0.0f, std::min(f, 1.0f)) * 255.0f);
+      }
+  return true;
+}
+
+// Watermark blend (renderer.cpp:637-655) into an RGB8 / RGBA8 face (Image3c / Image4c).
+static void apply_watermark(uint8_t* img, int width, int height, int fmt, size_t stride) {
+  static std::vector<uint8_t> wm;
+  static int ww = 0, wh = 0;
+  static bool loaded = false, ok = false;
+  if (!loaded) {
+    ok = load_watermark(wm, ww, wh);
+    loaded = true;
+  }
+  if (!ok || fmt >= 2) return;
+  const int bpp = fmt == 0 ? 3 : 4;
+  const float one_over_255 = 1.0f / 255.0f;
+  for (int y = 0; y < wh; ++y)
+    for (int x = 0; x < ww; ++x) {
+      const uint8_t* w4 = &wm[((size_t)y * ww + x) * 4];
+      const float wc[4] = {w4[0] * one_over_255, w4[1] * one_over_255, w4[2] * one_over_255, w4[3] * one_over_255};
+      const int xDst = (int)(x + (width - ww) * .5f);
+      const int yDst = (int)(y + (height - wh) * .5f);
+      if (xDst < 0 || xDst >= width || yDst < 0 || yDst >= height) continue;
+      uint8_t* p = img + (size_t)yDst * stride + (size_t)xDst * bpp;
+      for (int k = 0; k < 3; ++k) {
+        const float ic = p[k] * one_over_255;
+        const float b = (1.f - wc[3]) * ic + wc[3] * wc[k];
+        p[k] = (uint8_t)(std::max(0.0f, std::min(b, 1.0f)) * 255.0f);
+      }
+    }
+}
+
 void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outImage) {
   if (!renderer) throw std::runtime_error("no renderer set");
   const int fmt = fb_format(format);
   const size_t stride = fb_stride(fmt, width);
   YRTHandle sc = createScene();
   if (stereo) {
-    // non-FPR stereo branch (:742-878): 12 faces, strip = right eye first, each L,R,U,D,B,F
+    // stereo branch (renderer.cpp:742-878; DLL/FPR variant :543-737 adds the watermark):
+    // 12 faces, strip = right eye first, each eye L,R,U,D,B,F
     std::vector<std::vector<uint8_t>> faces(12);
+    static const char* kFaceName[6] = {"front", "right", "back", "left", "top", "bottom"};
+    const std::string base = fileName.empty() ? std::string() : fileName.substr(0, fileName.find_last_of('.'));
     for (int i = 0; i < 12; ++i) {
       YRTHandle cam = createCamera(i);
       check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
@@ -436,6 +516,15 @@ void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outI
       const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
       faces[i].assign(p, p + stride * height);
       check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+      // only the front, back and side faces carry the watermark (renderer.cpp:636-637)
+      if (fprOutput && waterMark && (i % 6) < 4) apply_watermark(faces[i].data(), width, height, fmt, stride);
+      if (debugging && !fileName.empty()) {
+        // <name>_<face>_image_<eye>.<ext> (renderer.cpp:763-799; FPR inserts the camera name)
+        const std::string faceFile = base + "_" + kFaceName[i % 6] + "_image_" + (i < 6 ? "left" : "right") +
+                                     (fprOutput ? std::string(".jpg") : "." + ext_of(fileName));
+        store_image(faceFile, width, height, fmt, faces[i].data(), stride, jpegQuality);
+        savedFiles.push_back(faceFile);
+      }
       if (stopFlag && stopFlag->load()) return;
     }
     const int bpp = fmt == 0 ? 3 : fmt == 1 ? 4 : fmt == 2 ? 12 : 16;
@@ -446,10 +535,18 @@ void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outI
       for (int seg = 0; seg < 12; ++seg) {
         const int eye = seg / 6 == 0 ? 1 : 0;
         const int face = 6 * eye + seg2face[seg % 6];
-        memcpy(&strip[(size_t)y * sstride + (size_t)seg * width * bpp], &faces[face][(size_t)y * stride],
-               (size_t)width * bpp);
+        uint8_t* dst = &strip[(size_t)y * sstride + (size_t)seg * width * bpp];
+        const uint8_t* src = &faces[face][(size_t)y * stride];
+        memcpy(dst, src, (size_t)width * bpp);
+        // finalImage->set(x, y, face->get(x, y)) round-trips bytes through Color4
+        if (fmt < 2)
+          for (int k = 0; k < width * bpp; ++k)
+            if (fmt == 0 || (k & 3) != 3) dst[k] = requant(dst[k]);
       }
-    if (!fileName.empty()) store_image(fileName, width * 12, height, fmt, strip.data(), sstride);
+    if (!fileName.empty()) {
+      store_image(fileName, width * 12, height, fmt, strip.data(), sstride, jpegQuality);
+      savedFiles.push_back(fileName);
+    }
     if (outImage) *outImage = strip;
   } else {
     YRTHandle cam = createCamera(-1);
@@ -459,7 +556,10 @@ void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outI
       check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
     for (int i = 0; i < numBuffers; i++) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
     const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
-    if (!fileName.empty()) store_image(fileName, width, height, fmt, p, stride);
+    if (!fileName.empty()) {
+      store_image(fileName, width, height, fmt, p, stride, jpegQuality);
+      savedFiles.push_back(fileName);
+    }
     if (outImage) outImage->assign(p, p + stride * height);
     check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
   }

@@ -105,6 +105,8 @@ struct RtState {
   std::string format = "RGB8";
   std::string outFileName;
   int numFrames = 1, jpegQuality = 90;
+  bool fprOutput = false;               // DLL (StartRT) output: watermark, .jpg faces
+  std::vector<std::string> savedFiles;  // files written by outputMode (StopRT cleanup)
   std::atomic<bool>* stopFlag = nullptr;
   void* statusCallback = nullptr;
   void* statusUser = nullptr;
@@ -118,6 +120,9 @@ struct RtState {
 };
 
 std::vector<std::string> tokenize_args(int argc, const char** argv);
-void store_image(const std::string& file, int w, int h, int format, const void* pixels, size_t stride);
+void store_image(const std::string& file, int w, int h, int format, const void* pixels, size_t stride,
+                 int quality = 90);
+// Baseline JPEG (jpeg_encode.cpp): 8-bit RGB, top row first
+std::vector<uint8_t> encode_jpeg(const uint8_t* rgb, int width, int height, size_t stride, int quality);
 
 }  // namespace yrtfe

@@ -117,6 +117,17 @@ int yrtSessionOutput(YRTSession s, const char* file) {
   }
 }
 
+int yrtStoreImage(const char* file, int width, int height, int format, const void* pixels, size_t stride,
+                  int quality) {
+  try {
+    store_image(file, width, height, format, pixels, stride, quality);
+    return 0;
+  } catch (const std::exception& e) {
+    g_feError = e.what();
+    return -1;
+  }
+}
+
 // embree::main (renderer.cpp:1406-1474)
 int yrtMain(int argc, const char** argv) {
   YRTSession s = yrtSessionCreate(nullptr, argc, argv);
@@ -207,9 +218,10 @@ bool StartRT(const char* colladaFile, const ParamsRT* params) {
   more.push_back(std::to_string(cur.zeroParallax));
   if (cur.debug) more.push_back("-debug");
   argv.insert(argv.end(), more.begin(), more.end());
-  // output: <dae-dir>/<name>.png next to the input (JPEG store: SURVEY §8(f) rank 2)
+  // output: <dir>/<name>_<camera>.jpg next to the input (renderer.cpp:719-720); scenes
+  // without Collada cameras use the camera name "cubemap"
   const std::string base = fn.substr(0, fn.find_last_of('.'));
-  const std::string out = base + "_cubemap.png";
+  const std::string out = base + "_cubemap.jpg";
   g_stop = false;
   g_running = true;
   g_worker = std::thread([argv, out, ext]() {
@@ -227,6 +239,7 @@ bool StartRT(const char* colladaFile, const ParamsRT* params) {
     }
     tracker_state(Rendering);
     g_numFaces = s->st.stereo ? 12 : 1;
+    s->st.fprOutput = true;
     try {
       std::vector<uint8_t> img;
       s->st.outputMode(g_stop ? std::string() : out, &img);
@@ -234,9 +247,12 @@ bool StartRT(const char* colladaFile, const ParamsRT* params) {
       fprintf(stderr, "StartRT: %s\n", e.what());
       tracker_error(UnknownError);
     }
+    const std::vector<std::string> saved = s->st.savedFiles;
     yrtSessionDestroy(s);
     if (g_stop) {
-      if (!g_keepResults) remove(out.c_str());
+      // StopRT(keepResults = false) removes every image written so far (renderer.cpp:724-731)
+      if (!g_keepResults)
+        for (const auto& f : saved) remove(f.c_str());
       tracker_state(Stopped);
     } else {
       tracker_state(Done);

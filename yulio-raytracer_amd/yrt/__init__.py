@@ -420,6 +420,16 @@ class Session:
             raise RuntimeError(N.fe.yrtFrontendLastError().decode())
 
 
+def store_image(file, img, quality=90):
+    """storeImage: numpy (H, W, 3|4) uint8 or float32 -> .jpg/.png/.ppm/.pfm."""
+    a = np.ascontiguousarray(img)
+    h, w, c = a.shape
+    fmt = {(np.dtype(np.uint8), 3): 0, (np.dtype(np.uint8), 4): 1, (np.dtype(np.float32), 3): 2,
+           (np.dtype(np.float32), 4): 3}[(a.dtype, c)]
+    if N.fe.yrtStoreImage(_b(str(file)), w, h, fmt, a.ctypes.data, a.strides[0], int(quality)) != 0:
+        raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+
+
 # ---- DLL API (YulioRT.h)
 def InitParamsRT() -> ParamsRT:
     p = ParamsRT()

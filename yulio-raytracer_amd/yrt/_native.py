@@ -157,6 +157,7 @@ _sig(fe, "yrtSessionCamera", vp, vp, i32)
 _sig(fe, "yrtSessionRender", vp, vp, i32)
 _sig(fe, "yrtSessionOutput", i32, vp, cstr)
 _sig(fe, "yrtMain", i32, i32, C.POINTER(cstr))
+_sig(fe, "yrtStoreImage", i32, cstr, i32, i32, i32, vp, sz, i32)
 _sig(fe, "InitParamsRT", None, C.POINTER(ParamsRT))
 _sig(fe, "StartRT", C.c_bool, cstr, C.POINTER(ParamsRT))
 _sig(fe, "WaitRT", C.c_bool)
