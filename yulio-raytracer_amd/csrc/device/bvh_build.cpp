@@ -55,6 +55,9 @@ struct Builder {
 #define YRT_MAX_LEAF 8
 #endif
   int maxLeaf = YRT_MAX_LEAF;
+#ifndef YRT_SAH_TRAV
+#define YRT_SAH_TRAV 1.0f  // SAH cost of a traversal step relative to one triangle test
+#endif
   int medianDepth = 24;
   int maxDepthSeen = 0;
 
@@ -124,7 +127,7 @@ struct Builder {
     }
     const float parentArea = bounds(b, e).area();
     const float leafCost = (float)n;
-    const float splitCost = 1.0f + (parentArea > 0.f ? bestCost / parentArea : (float)n);
+    const float splitCost = YRT_SAH_TRAV + (parentArea > 0.f ? bestCost / parentArea : (float)n);
     if (n <= maxLeaf && leafCost <= splitCost) { makeLeaf = true; return e; }
     if (bestAxis < 0) return b + n / 2;
     const float lo = cb.lo[bestAxis], hi = cb.hi[bestAxis];

@@ -285,6 +285,9 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 4  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
+#ifndef YRT_NODE_LOOP
+#define YRT_NODE_LOOP 1  // +1.5 % on C3 (node steps chained without the refill block)
+#endif
 #ifndef YRT_TRACE_WAVES
 #define YRT_TRACE_WAVES 6
 #endif
@@ -415,6 +418,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     const int nNode = __popcll(__ballot(has && curCnt == 0));
     const int nBlocked = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
     if (nNode * 4 > nBlocked * YRT_NODE_BIAS) {
+#if YRT_NODE_LOOP
+     // consecutive node steps without the retire/refill block in between
+     while (true) {
+#endif
       YRT_PROF(2, 1);
       YRT_PROF(3, __popcll(__ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
@@ -439,6 +446,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
       }
+#if YRT_NODE_LOOP
+      const int nNode2 = __popcll(__ballot(has && curCnt == 0));
+      const int nBlocked2 = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
+      if (!(nNode2 * 4 > nBlocked2 * YRT_NODE_BIAS)) break;
+     }
+#endif
     } else {
       // leaf step: the parked leaf, or else the current entry when it is a leaf
       const bool usePend = pendCnt > 0;
