@@ -37,10 +37,19 @@ YRT_API int yrtSessionInfo(YRTSession s, YRTSessionInfo* out);
 /* Camera of the session: face -1 = mono pinhole (createCamera), 0..11 = stereo cube faces
  * (renderer.cpp:747-757). The handle is owned by the session. */
 YRT_API YRTHandle yrtSessionCamera(YRTSession s, int face);
+/* Stereo cube cameras a Collada scene created: 12 per FPR view, in DAELoader order
+ * (devices/device/loaders/ColladaLoader.cpp:402-505). */
+YRT_API int yrtSessionNumSceneCameras(YRTSession s);
+YRT_API YRTHandle yrtSessionSceneCamera(YRTSession s, int i);
+/* One FPR face of scene camera i (renderer.cpp:548-576): faceCamera primitives re-oriented
+ * toward the camera origin, scene re-committed, frame rendered; returns the mapped
+ * framebuffer (format per yrtSessionInfo). */
+YRT_API void* yrtSessionRenderSceneCamera(YRTSession s, int i);
 /* Renders one frame (mono: face -1) into the session framebuffer and returns the mapped
  * host pointer (format per yrtSessionInfo). */
 YRT_API void* yrtSessionRender(YRTSession s, int face);
-/* outputMode(-o file): renders and stores the image (.ppm/.pfm/.png; stereo: 12-face strip). */
+/* outputMode(-o file): renders and stores the image (.ppm/.pfm/.png; stereo: 12-face strip;
+ * with Collada cameras the FPR branch: <dir>/<name>_<camera>.jpg per view, file ignored). */
 YRT_API int yrtSessionOutput(YRTSession s, const char* file);
 
 /* storeImage (common/image/image.cpp:77-104): .jpg (baseline, quality 1..100, the FreeImage

@@ -102,11 +102,3 @@ def test_startrt_writes_cubemap_jpeg(tmp_path):
     # strip segments L,R,U,D,B,F per eye: U and D (2,3 / 8,9) carry no watermark
     assert all(diff[k] > 0 for k in (0, 1, 4, 5, 6, 7, 10, 11)), diff
     assert all(diff[k] <= 2 for k in (2, 3, 8, 9)), diff
-
-
-def test_startrt_rejects_collada_until_supported(tmp_path):
-    f = tmp_path / "x.dae"
-    f.write_text("<COLLADA/>")
-    assert yrt.StartRT(f)
-    yrt.WaitRT()
-    assert yrt.GetLastErrorRT() == 3  # InvalidColladaFormat

@@ -133,9 +133,24 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
     } else if (tag == "-debug") {
       debugging = true;
     } else if (tag == "-i") {
+      // rtLoadScene(g_sceneFileName, &g_stereoCubeCameras, g_faceCullingMode) (:1002-1006)
       const std::string file = join_path(path, cin.get());
-      auto p = loader->loadScene(file);
+      sceneFileName = file;
+      std::vector<YRTHandle> p;
+      if (ext_of(file) == "dae") {
+        p = load_dae(*loader, file, faceCullingMode, &stereoCubeCameras);
+        loader->images.clear();
+        loader->textures.clear();
+        // DLL / FPR path: g_sceneScale from the first camera before the options are parsed
+        // (renderer.cpp:1453-1456, 1504)
+        if (fprCollada && !stereoCubeCameras.empty())
+          check(dev, yrtGetFloat1(dev, stereoCubeCameras[0], "sceneScale", &sceneScale), "rtGetFloat1");
+      } else {
+        p = loader->loadScene(file);
+      }
       prims.insert(prims.end(), p.begin(), p.end());
+    } else if (tag == "-fprCollada") {
+      fprCollada = true;
     } else if (tag == "-trisphere") {
       YRTHandle s = checkH(dev, yrtNewShape(dev, "sphere"), "rtNewShape");
       const yrt_v3 P = cin.getV3();
@@ -498,18 +513,112 @@ static void apply_watermark(uint8_t* img, int width, int height, int fmt, size_t
     }
 }
 
+std::vector<uint8_t> assemble_strip(const std::vector<std::vector<uint8_t>>& faces, int width, int height, int fmt,
+                                    size_t stride);
+
+void RtState::renderFprFace(size_t i) {
+  YRTHandle sc = createScene();
+  YRTHandle cam = stereoCubeCameras.at(i);
+  // update the dynamic geometry (self-aligning instances) for this view (:550-559)
+  float camPos[3], up[3] = {camUp.x, camUp.y, camUp.z};
+  check(dev, yrtGetFloat3(dev, cam, "origin", &camPos[0], &camPos[1], &camPos[2]), "rtGetFloat3");
+  for (size_t j = 0; j < prims.size(); ++j)
+    check(dev, yrtUpdatePrimitive(dev, sc, j, prims[j], camPos, up), "rtUpdatePrimitive");
+  check(dev, yrtCommit(dev, sc), "rtCommit(scene)");
+  if (toeIn) {  // :569-574
+    check(dev, yrtSetBool1(dev, cam, "toeIn", 1), "rtSetBool1");
+    check(dev, yrtCommit(dev, cam), "rtCommit(camera)");
+  }
+  check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
+  for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
+}
+
+void RtState::fprOutputMode() {
+  const size_t numViews = stereoCubeCameras.size();
+  if (onStage) onStage(0, (int)numViews);
+  // the cube faces must be square (:528-532)
+  if (width != height) {
+    width = height = std::max(width, height);
+    frameBuffer = checkH(dev, yrtNewFrameBuffer(dev, format.c_str(), width, height, numBuffers, nullptr), "rtNewFrameBuffer");
+  }
+  const int fmt = fb_format(format);
+  const size_t stride = fb_stride(fmt, width);
+  static const char* kFaceName[6] = {"front", "right", "back", "left", "top", "bottom"};
+  // <path>\<name>_<camera>... (:584-586, 719-720)
+  const std::string dir = path_of(sceneFileName);
+  std::string base = sceneFileName.substr(dir.size());
+  base = base.substr(0, base.find_last_of('.'));
+  std::vector<std::vector<uint8_t>> faces;
+  for (size_t i = 0; i < numViews && !(stopFlag && stopFlag->load()); ++i) {
+    if (onStage) onStage((int)i, (int)numViews);
+    const size_t cubeFaceIndex = i % 12;
+    if (cubeFaceIndex == 0) faces.clear();
+    char nameBuf[1024];
+    int n = yrtGetString(dev, stereoCubeCameras[i], "name", nameBuf, sizeof(nameBuf));
+    const std::string cameraName = n >= 0 ? std::string(nameBuf) : std::string();
+    renderFprFace(i);
+    const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
+    faces.emplace_back(p, p + stride * height);
+    check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+    if (waterMark && (cubeFaceIndex % 6) < 4) apply_watermark(faces.back().data(), width, height, fmt, stride);
+    const std::string faceFile = dir + base + "_" + cameraName + "_" + kFaceName[cubeFaceIndex % 6] + "_image_" +
+                                 (cubeFaceIndex < 6 ? "left" : "right") + ".jpg";
+    if (debugging) {
+      store_image(faceFile, width, height, fmt, faces.back().data(), stride, jpegQuality);
+      savedFiles.push_back(faceFile);
+    }
+    if (cubeFaceIndex == 11) {
+      std::vector<uint8_t> strip = assemble_strip(faces, width, height, fmt, stride);
+      const int bpp = fmt == 0 ? 3 : fmt == 1 ? 4 : fmt == 2 ? 12 : 16;
+      store_image(dir + base + "_" + cameraName + ".jpg", width * 12, height, fmt, strip.data(),
+                  (size_t)bpp * width * 12, jpegQuality);
+      // the reference records the last face's file name here, not the strip's (:716), so
+      // StopRT(false) never removes a finished strip
+      savedFiles.push_back(faceFile);
+    }
+  }
+}
+
+// strip = right eye first, each eye L,R,U,D,B,F (renderer.cpp:663-715, 820-877); bytes go
+// through Color4 (finalImage->set(x, y, face->get(x, y)))
+std::vector<uint8_t> assemble_strip(const std::vector<std::vector<uint8_t>>& faces, int width, int height, int fmt,
+                                    size_t stride) {
+  const int bpp = fmt == 0 ? 3 : fmt == 1 ? 4 : fmt == 2 ? 12 : 16;
+  const size_t sstride = (size_t)bpp * width * 12;
+  std::vector<uint8_t> strip(sstride * height);
+  static const int seg2face[6] = {3, 1, 4, 5, 2, 0};
+  for (int y = 0; y < height; ++y)
+    for (int seg = 0; seg < 12; ++seg) {
+      const int eye = seg / 6 == 0 ? 1 : 0;
+      const int face = 6 * eye + seg2face[seg % 6];
+      uint8_t* dst = &strip[(size_t)y * sstride + (size_t)seg * width * bpp];
+      const uint8_t* src = &faces[face][(size_t)y * stride];
+      memcpy(dst, src, (size_t)width * bpp);
+      if (fmt < 2)
+        for (int k = 0; k < width * bpp; ++k)
+          if (fmt == 0 || (k & 3) != 3) dst[k] = requant(dst[k]);
+    }
+  return strip;
+}
+
 void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outImage) {
   if (!renderer) throw std::runtime_error("no renderer set");
+  if (stereo && !stereoCubeCameras.empty()) {
+    fprOutputMode();
+    return;
+  }
   const int fmt = fb_format(format);
   const size_t stride = fb_stride(fmt, width);
   YRTHandle sc = createScene();
   if (stereo) {
+    if (onStage) onStage(0, 12);
     // stereo branch (renderer.cpp:742-878; DLL/FPR variant :543-737 adds the watermark):
     // 12 faces, strip = right eye first, each eye L,R,U,D,B,F
     std::vector<std::vector<uint8_t>> faces(12);
     static const char* kFaceName[6] = {"front", "right", "back", "left", "top", "bottom"};
     const std::string base = fileName.empty() ? std::string() : fileName.substr(0, fileName.find_last_of('.'));
     for (int i = 0; i < 12; ++i) {
+      if (onStage) onStage(i, 12);
       YRTHandle cam = createCamera(i);
       check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
       for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
@@ -529,20 +638,7 @@ void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outI
     }
     const int bpp = fmt == 0 ? 3 : fmt == 1 ? 4 : fmt == 2 ? 12 : 16;
     const size_t sstride = (size_t)bpp * width * 12;
-    std::vector<uint8_t> strip(sstride * height);
-    static const int seg2face[6] = {3, 1, 4, 5, 2, 0};
-    for (int y = 0; y < height; ++y)
-      for (int seg = 0; seg < 12; ++seg) {
-        const int eye = seg / 6 == 0 ? 1 : 0;
-        const int face = 6 * eye + seg2face[seg % 6];
-        uint8_t* dst = &strip[(size_t)y * sstride + (size_t)seg * width * bpp];
-        const uint8_t* src = &faces[face][(size_t)y * stride];
-        memcpy(dst, src, (size_t)width * bpp);
-        // finalImage->set(x, y, face->get(x, y)) round-trips bytes through Color4
-        if (fmt < 2)
-          for (int k = 0; k < width * bpp; ++k)
-            if (fmt == 0 || (k & 3) != 3) dst[k] = requant(dst[k]);
-      }
+    std::vector<uint8_t> strip = assemble_strip(faces, width, height, fmt, stride);
     if (!fileName.empty()) {
       store_image(fileName, width * 12, height, fmt, strip.data(), sstride, jpegQuality);
       savedFiles.push_back(fileName);

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -107,6 +108,12 @@ struct RtState {
   int numFrames = 1, jpegQuality = 90;
   bool fprOutput = false;               // DLL (StartRT) output: watermark, .jpg faces
   std::vector<std::string> savedFiles;  // files written by outputMode (StopRT cleanup)
+  // Collada / FPR state (renderer.cpp:250-256, 1410-1460): the stereo cube cameras a .dae
+  // scene created (12 per FPR view) and the file they were loaded from
+  bool fprCollada = false;              // DLL / single-.dae main: sceneScale taken from the cameras
+  std::string sceneFileName;
+  std::vector<YRTHandle> stereoCubeCameras;
+  std::function<void(int, int)> onStage;  // YulioStatusTracker::Init/SetCurrentStage
   std::atomic<bool>* stopFlag = nullptr;
   void* statusCallback = nullptr;
   void* statusUser = nullptr;
@@ -117,7 +124,17 @@ struct RtState {
   YRTHandle createCamera(int face);
   YRTHandle createScene();
   void outputMode(const std::string& file, std::vector<uint8_t>* outImage = nullptr);
+  // FPR branch of outputMode (renderer.cpp:519-737): per camera view, update faceCamera
+  // primitives, render the 12 faces, store <dir>/<name>_<camera>.jpg
+  void fprOutputMode();
+  // one FPR face: faceCamera update + scene commit + render (renderer.cpp:548-576)
+  void renderFprFace(size_t i);
 };
+
+// Collada scene (collada.cpp): primitives in DAELoader order; *cameras receives the 12
+// stereo cube cameras per FPR view (DAELoader::initSceneCameras)
+std::vector<YRTHandle> load_dae(Loader& L, const std::string& file, const std::string& faceCullingMode,
+                                std::vector<YRTHandle>* cameras);
 
 std::vector<std::string> tokenize_args(int argc, const char** argv);
 void store_image(const std::string& file, int w, int h, int format, const void* pixels, size_t stride,

@@ -3,7 +3,7 @@
 //   rtLoadImage / rtLoadTexture caches     devices/device/loaders/loaders.cpp:27-66
 //   XML scene loader                       devices/device/loaders/xml_loader.cpp:274-620
 //   OBJ + MTL loader                       devices/device/loaders/obj_loader.cpp:28-411
-// Collada (.dae, via the modified Assimp) is SURVEY §8(f) rank 1 and not part of this build.
+// Collada (.dae): collada.cpp.
 #include "frontend.h"
 
 #include <ctype.h>
@@ -651,7 +651,7 @@ std::vector<YRTHandle> Loader::loadScene(const std::string& file) {
     XMLLoader l(*this, file);
     prims = l.model;
   } else if (ext == "dae") {
-    throw std::runtime_error("Collada (.dae) loading is not part of this build yet (SURVEY.md §8(f) rank 1)");
+    prims = load_dae(*this, file, "default", nullptr);  // cameras: see RtState "-i
   } else {
     throw std::runtime_error("unknown scene file format: " + file);
   }

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -82,6 +83,27 @@ int yrtSessionInfo(YRTSession s, YRTSessionInfo* out) {
   } catch (const std::exception& e) {
     g_feError = e.what();
     return -1;
+  }
+}
+
+int yrtSessionNumSceneCameras(YRTSession s) { return (int)s->st.stereoCubeCameras.size(); }
+
+YRTHandle yrtSessionSceneCamera(YRTSession s, int i) {
+  if (i < 0 || (size_t)i >= s->st.stereoCubeCameras.size()) {
+    g_feError = "scene camera index out of range";
+    return nullptr;
+  }
+  return s->st.stereoCubeCameras[i];
+}
+
+void* yrtSessionRenderSceneCamera(YRTSession s, int i) {
+  try {
+    RtState& st = s->st;
+    st.renderFprFace((size_t)i);
+    return yrtMapFrameBuffer(st.dev, st.frameBuffer, -1);
+  } catch (const std::exception& e) {
+    g_feError = e.what();
+    return nullptr;
   }
 }
 
@@ -198,9 +220,13 @@ bool StartRT(const char* colladaFile, const ParamsRT* params) {
   }
   ParamsRT cur;
   if (params) cur = *params;
-  // argv synthesis (renderer.cpp:1557-1585)
+  // argv synthesis (renderer.cpp:1557-1585). A .dae is loaded first, with the culling mode
+  // of the parameters and g_sceneScale taken from its cameras (workerThreadRT :1494-1505);
+  // .ecs/.xml/.obj scenes (an extension of this build) go through the same command line.
   std::vector<std::string> argv;
   if (ext == "ecs") argv = {"-c", fn};
+  else if (ext == "dae")
+    argv = {"-fprCollada", "-faceCullingMode", cur.faceCullingMode ? cur.faceCullingMode : "default", "-i", fn};
   else argv = {"-i", fn};
   const char* rend = cur.renderer ? cur.renderer : "pathtracer";
   std::vector<std::string> more = {"-stereo", "-renderer", rend, "-spp", std::to_string(cur.spp), "-size",
@@ -225,20 +251,29 @@ bool StartRT(const char* colladaFile, const ParamsRT* params) {
   g_stop = false;
   g_running = true;
   g_worker = std::thread([argv, out, ext]() {
-    if (ext == "dae") {
-      tracker_error(InvalidColladaFormat);  // Collada: SURVEY §8(f) rank 1
-      tracker_state(Done);
-      return;
-    }
     YRTSession s = session_new(nullptr, argv, &g_stop, (void*)&status_cb, nullptr, "");
     if (!s) {
       fprintf(stderr, "StartRT: %s\n", yrtFrontendLastError());
-      tracker_error(UnknownError);
+      // a Collada file the loader rejects, or one without cameras (:1497-1500)
+      tracker_error(ext == "dae" ? InvalidColladaFormat : UnknownError);
+      tracker_state(Done);
+      return;
+    }
+    if (ext == "dae" && (s->st.stereoCubeCameras.empty() || s->st.prims.empty())) {
+      tracker_error(InvalidColladaFormat);
+      yrtSessionDestroy(s);
       tracker_state(Done);
       return;
     }
     tracker_state(Rendering);
+    g_faceIndex = 0;
     g_numFaces = s->st.stereo ? 12 : 1;
+    s->st.onStage = [](int stage, int numStages) {
+      std::lock_guard<std::mutex> g(g_trackerMu);
+      g_faceIndex = stage;
+      g_numFaces = numStages;
+      g_status.progress = float(stage) / float(std::max(1, numStages));
+    };
     s->st.fprOutput = true;
     try {
       std::vector<uint8_t> img;

@@ -411,9 +411,29 @@ class Session:
         N.dev.yrtUnmapFrameBuffer(self.device.h, i["framebuffer"], -1)
         return self.device.framebuffer_array(i["framebuffer"], i["width"], i["height"], fmt)
 
-    def export_frame(self, face=-1) -> bytes:
+    def export_frame(self, face=-1, camera=None) -> bytes:
         i = self.info()
-        return self.device.export_frame(i["renderer"], self.camera(face), i["scene"])
+        return self.device.export_frame(i["renderer"], camera if camera else self.camera(face), i["scene"])
+
+    # -- Collada scenes: stereo cube cameras of the FPR views (12 per view)
+    def num_scene_cameras(self) -> int:
+        return int(N.fe.yrtSessionNumSceneCameras(self.h))
+
+    def scene_camera(self, i):
+        h = N.fe.yrtSessionSceneCamera(self.h, i)
+        if not h:
+            raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+        return h
+
+    def render_scene_camera(self, i):
+        """One FPR face (faceCamera update, scene commit, render) of scene camera i."""
+        p = N.fe.yrtSessionRenderSceneCamera(self.h, i)
+        if not p:
+            raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+        info = self.info()
+        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[info["framebufferFormat"]]
+        N.dev.yrtUnmapFrameBuffer(self.device.h, info["framebuffer"], -1)
+        return self.device.framebuffer_array(info["framebuffer"], info["width"], info["height"], fmt)
 
     def output(self, file=None):
         if N.fe.yrtSessionOutput(self.h, _b(file) if file else None) != 0:

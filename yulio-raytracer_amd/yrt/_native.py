@@ -155,6 +155,9 @@ _sig(fe, "yrtFrontendLastError", cstr)
 _sig(fe, "yrtSessionInfo", i32, vp, C.POINTER(SessionInfo))
 _sig(fe, "yrtSessionCamera", vp, vp, i32)
 _sig(fe, "yrtSessionRender", vp, vp, i32)
+_sig(fe, "yrtSessionNumSceneCameras", i32, vp)
+_sig(fe, "yrtSessionSceneCamera", vp, vp, i32)
+_sig(fe, "yrtSessionRenderSceneCamera", vp, vp, i32)
 _sig(fe, "yrtSessionOutput", i32, vp, cstr)
 _sig(fe, "yrtMain", i32, i32, C.POINTER(cstr))
 _sig(fe, "yrtStoreImage", i32, cstr, i32, i32, i32, vp, sz, i32)
