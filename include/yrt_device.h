@@ -168,6 +168,11 @@ YRT_API int yrtSetFrameSeed(YRTDevice dev, uint32_t seed);
 YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
 /* Tile sharding for multi-GPU: render only tiles with (tileIndex % count) == index. */
 YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
+/* Scene commits that only move the vertices of some primitives (faceCamera re-orientation by
+ * rtUpdatePrimitive, the FPR loop of renderer.cpp:550-559) refit the BVH on the GPU instead of
+ * rebuilding it (on by default). yrtGetSceneRefits: refit commits since the last rebuild. */
+YRT_API int yrtSetRefitCommits(YRTDevice dev, int on);
+YRT_API int yrtGetSceneRefits(YRTDevice dev, YRTHandle scene);
 /* Host sampler check: writes the SoA sample table (dims x (sets*spp)) that the frame
  * renderer uploads (sampler/sampler.cpp:46-126 restated); returns sets*spp records. */
 /* Ray capture for the roofline's algorithmic bytes: while maxPerDepth > 0,

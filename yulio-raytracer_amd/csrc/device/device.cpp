@@ -44,6 +44,7 @@ class Device {
   uint32_t frameSeed = 0x2545F491u;
   int64_t capacity = 16ll << 20;
   int shardIndex = 0, shardCount = 1;
+  bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
   bool kernelTiming = false;
   YRTRenderStats stats{};
   // ray capture (roofline accounting): strided sample of each depth's query streams, batch 0
@@ -410,7 +411,14 @@ void Device::intersect(SceneObj& S, const float* org4, const float* dir4, uint32
 // ---------------------------------------------------------------- scene commit
 void SceneObj::commit() {
   std::vector<std::shared_ptr<ScenePrim>> prims = slots;
-  gpu = build_gpu_scene(prims, YRT_STACK_DEPTH, static_cast<Device*>(dev)->gpu);
+  Device* d = static_cast<Device*>(dev);
+  // per-face commits of the FPR loop (renderer.cpp:550-559) only re-orient faceCamera
+  // meshes: refit on the GPU instead of rebuilding
+  if (gpu && d->gpu && d->refitCommits) {
+    HIP_CHECK(hipSetDevice(d->hipDevice));
+    if (refit_gpu_scene(*gpu, prims, d->stream)) return;
+  }
+  gpu = build_gpu_scene(prims, YRT_STACK_DEPTH, d->gpu);
 }
 
 }  // namespace yrt
@@ -1048,6 +1056,7 @@ int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes,
   DEV_GUARD(dev, -1)
   auto S = dev->d->get<SceneObj>(scene, "scene");
   if (!S->gpu) throw std::runtime_error("scene not committed");
+  sync_host_bvh(*S->gpu);
   const size_t nb = S->gpu->hNodes.size() * sizeof(GpuNode), tb = S->gpu->hTris.size() * sizeof(GpuTri);
   if (nodesBytes < nb || trisBytes < tb) throw std::runtime_error("buffers too small");
   memcpy(nodes, S->gpu->hNodes.data(), nb);
@@ -1169,6 +1178,21 @@ int yrtSetTileShard(YRTDevice dev, int index, int count) {
   dev->d->shardIndex = index;
   dev->d->shardCount = count;
   return 0;
+  DEV_END(-1)
+}
+
+int yrtSetRefitCommits(YRTDevice dev, int on) {
+  DEV_GUARD(dev, -1)
+  dev->d->refitCommits = on != 0;
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtGetSceneRefits(YRTDevice dev, YRTHandle scene) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!S || !S->gpu) throw std::runtime_error("scene not committed");
+  return S->gpu->refits;
   DEV_END(-1)
 }
 

@@ -235,12 +235,97 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   v.numNodes = (int)bvh.nodes.size();
   v.numTris = gidBase;
 
+  // refit support: slot -> geometry, gid -> leaf position, nodes grouped by depth
+  S->slotsCommitted = prims;
+  S->slotGeom.assign(prims.size(), -1);
+  {
+    int gcount = 0;
+    for (size_t i = 0; i < prims.size(); ++i)
+      if (prims[i] && prims[i]->shape) S->slotGeom[i] = gcount++;
+    std::vector<int> leafOf(gidBase);
+    for (int i = 0; i < gidBase; ++i) leafOf[bvh.order[i]] = i;
+    S->triLeaf.upload(leafOf);
+    std::vector<std::vector<int>> levels;
+    std::vector<std::pair<int, int>> work = {{0, 0}};
+    for (size_t w = 0; w < work.size(); ++w) {
+      const int ni = work[w].first, d = work[w].second;
+      if ((int)levels.size() <= d) levels.resize(d + 1);
+      levels[d].push_back(ni);
+      for (int k = 0; k < 4; ++k) {
+        const int c = bvh.nodes[ni].child[k];
+        if (c != -1 && (c & 31) == 0) work.push_back({c >> 5, d + 1});
+      }
+    }
+    std::vector<int> flat;
+    S->levelStart.clear();
+    for (auto& l : levels) {
+      S->levelStart.push_back((int)flat.size());
+      flat.insert(flat.end(), l.begin(), l.end());
+    }
+    S->levelStart.push_back((int)flat.size());
+    S->levelNodes.upload(flat);
+  }
+
   S->hNodes = std::move(bvh.nodes);
   S->hTris = std::move(bvh.tris);
   S->hGeoms = geoms;
   S->hTriGeom = triGeom;
   S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return S;
+}
+
+bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>& prims, hipStream_t stream) {
+  if (!S.nodes.p || prims.size() != S.slotsCommitted.size() || S.hNodes.empty()) return false;
+  std::vector<size_t> moved;
+  for (size_t i = 0; i < prims.size(); ++i) {
+    const auto& o = S.slotsCommitted[i];
+    const auto& n = prims[i];
+    if (o == n) continue;
+    if (!o || !n || !o->shape || !n->shape || o->light || n->light) return false;
+    if (o->material != n->material || o->illumMask != n->illumMask || o->shadowMask != n->shadowMask) return false;
+    const MeshInst& a = *o->shape;
+    const MeshInst& b = *n->shape;
+    if (a.kind != b.kind || b.kind == GEOM_TRIANGLE || a.cull != b.cull) return false;
+    if (a.pos.size() != b.pos.size() || a.nor.size() != b.nor.size() || a.uv != b.uv || a.tri != b.tri) return false;
+    const bool same = !memcmp(a.pos.data(), b.pos.data(), a.pos.size() * sizeof(V3)) &&
+                      (a.nor.empty() || !memcmp(a.nor.data(), b.nor.data(), a.nor.size() * sizeof(V3)));
+    if (!same) moved.push_back(i);
+  }
+  S.slotsCommitted = prims;  // unchanged geometry: adopt the new slot objects (export)
+  if (moved.empty()) return true;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t i : moved) {
+    const MeshInst& m = *prims[i]->shape;
+    const GpuGeom& g = S.hGeoms[S.slotGeom[i]];
+    std::vector<float4> pos(m.pos.size()), nor(m.pos.size());
+    for (size_t k = 0; k < m.pos.size(); ++k) {
+      pos[k] = make_float4(m.pos[k].x, m.pos[k].y, m.pos[k].z, 0.f);
+      nor[k] = m.nor.empty() ? make_float4(0.f, 0.f, 0.f, 0.f) : make_float4(m.nor[k].x, m.nor[k].y, m.nor[k].z, 0.f);
+    }
+    HIP_CHECK(hipMemcpyAsync(S.positions.as<float4>() + g.vtxBase, pos.data(), pos.size() * sizeof(float4),
+                             hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemcpyAsync(S.normals.as<float4>() + g.vtxBase, nor.data(), nor.size() * sizeof(float4),
+                             hipMemcpyHostToDevice, stream));
+    launch_refit_tris(S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(), S.triLeaf.as<int>(),
+                      g.triBase, (int)(m.tri.size() / 3), stream);
+    // the host copies must outlive the async copies
+    HIP_CHECK(hipStreamSynchronize(stream));
+  }
+  for (int d = (int)S.levelStart.size() - 2; d >= 0; --d)
+    launch_refit_nodes(S.nodes.as<GpuNode>(), S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(),
+                       S.levelNodes.as<int>() + S.levelStart[d], S.levelStart[d + 1] - S.levelStart[d], stream);
+  HIP_CHECK(hipStreamSynchronize(stream));
+  S.hostBvhStale = true;
+  S.refits++;
+  S.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return true;
+}
+
+void sync_host_bvh(GpuScene& S) {
+  if (!S.hostBvhStale) return;
+  HIP_CHECK(hipMemcpy(S.hNodes.data(), S.nodes.p, S.hNodes.size() * sizeof(GpuNode), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(S.hTris.data(), S.tris.p, S.hTris.size() * sizeof(GpuTri), hipMemcpyDeviceToHost));
+  S.hostBvhStale = false;
 }
 
 }  // namespace yrt

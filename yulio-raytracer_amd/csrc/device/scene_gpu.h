@@ -63,6 +63,14 @@ struct GpuScene {
   std::vector<int> hTriGeom;
   std::vector<std::shared_ptr<const LightInst>> allLights;
   std::vector<LightSampleSource> precomputed;   // LightSampleSource per precompute() light
+  // incremental commits (faceCamera refit, refit_gpu_scene): the slots this scene was built
+  // from, slot -> geometry, gid -> leaf position, and the node indices grouped by tree depth
+  std::vector<std::shared_ptr<ScenePrim>> slotsCommitted;
+  std::vector<int> slotGeom;
+  std::vector<int> levelStart;  // nodes of depth d: levelNodes[levelStart[d] .. levelStart[d+1])
+  DevBuf triLeaf, levelNodes;
+  bool hostBvhStale = false;    // hNodes/hTris lag a device refit until sync_host_bvh
+  int refits = 0;               // refit commits since the build (stats)
   int numTris = 0, numGeoms = 0, bvhDepth = 0;
   double buildSeconds = 0;
   float bboxLo[3] = {0, 0, 0}, bboxHi[3] = {0, 0, 0};
@@ -70,5 +78,11 @@ struct GpuScene {
 
 std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<ScenePrim>>& prims, int stackDepth,
                                           bool upload);
+// Commits `prims` onto an uploaded scene without a rebuild when only vertex positions/normals
+// of some primitives changed (faceCamera re-orientation): uploads the moved vertices and
+// refits the BVH on the GPU. Returns false (scene untouched) when a rebuild is needed.
+bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>& prims, hipStream_t stream);
+// Brings the host BVH mirrors (export, stats) up to date after device refits.
+void sync_host_bvh(GpuScene& S);
 
 }  // namespace yrt

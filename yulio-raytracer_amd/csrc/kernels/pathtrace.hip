@@ -1221,3 +1221,82 @@ void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth,
 }
 
 }  // namespace yrt
+
+namespace yrt {
+
+// ---------------------------------------------------------------- BVH refit (faceCamera)
+// Per-face dynamic geometry (rtUpdatePrimitive of YULIO_CAMERA_ALIGNED_ meshes,
+// singleray_device.cpp:354-398) keeps the BVH topology and only moves vertices: the moved
+// triangles' Moeller-Trumbore records are rewritten from the new world vertices, then the
+// node boxes are refit bottom-up, one launch per tree level (deepest first). The reference
+// rebuilt the whole Embree BVH on every face commit. Boxes stay the exact
+// union of the original vertex bounds (what the builder computes), so the hits are identical
+// to a rebuild's: the closest hit is the smallest (t, triangle id) whatever the tree.
+__global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ tris, const int4* __restrict__ indices,
+                                                         const float4* __restrict__ positions,
+                                                         const int* __restrict__ triLeaf, int firstTri, int numTris) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= numTris) return;
+  const int gid = firstTri + i;
+  const int4 ix = indices[gid];
+  const float4 a = positions[ix.x], b = positions[ix.y], c = positions[ix.z];
+  GpuTri& t = tris[triLeaf[gid]];
+  // e1 = v0 - v1, e2 = v2 - v0 (device/bvh_build.cpp, rtcore convention); .w words kept
+  t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z;
+  t.e1[0] = a.x - b.x; t.e1[1] = a.y - b.y; t.e1[2] = a.z - b.z;
+  t.e2[0] = c.x - a.x; t.e2[1] = c.y - a.y; t.e2[2] = c.z - a.z;
+}
+
+__global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes(GpuNode* __restrict__ nodes, const GpuTri* __restrict__ tris,
+                                                          const int4* __restrict__ indices,
+                                                          const float4* __restrict__ positions,
+                                                          const int* __restrict__ levelNodes, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  GpuNode& n = nodes[levelNodes[i]];
+  for (int k = 0; k < 4; ++k) {
+    const int c = n.child[k];
+    if (c == -1) continue;
+    const int idx = c >> 5, cnt = c & 31;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (cnt > 0) {
+      for (int t = 0; t < cnt; ++t) {
+        const int gid = __float_as_int(tris[idx + t].v0[3]);
+        const int4 ix = indices[gid];
+        const float4 p[3] = {positions[ix.x], positions[ix.y], positions[ix.z]};
+        for (int v = 0; v < 3; ++v) {
+          lo[0] = fminf(lo[0], p[v].x); hi[0] = fmaxf(hi[0], p[v].x);
+          lo[1] = fminf(lo[1], p[v].y); hi[1] = fmaxf(hi[1], p[v].y);
+          lo[2] = fminf(lo[2], p[v].z); hi[2] = fmaxf(hi[2], p[v].z);
+        }
+      }
+    } else {
+      const GpuNode& ch = nodes[idx];
+      for (int j = 0; j < 4; ++j) {
+        if (ch.child[j] == -1) continue;
+        lo[0] = fminf(lo[0], ch.lox[j]); hi[0] = fmaxf(hi[0], ch.hix[j]);
+        lo[1] = fminf(lo[1], ch.loy[j]); hi[1] = fmaxf(hi[1], ch.hiy[j]);
+        lo[2] = fminf(lo[2], ch.loz[j]); hi[2] = fmaxf(hi[2], ch.hiz[j]);
+      }
+    }
+    n.lox[k] = lo[0]; n.hix[k] = hi[0];
+    n.loy[k] = lo[1]; n.hiy[k] = hi[1];
+    n.loz[k] = lo[2]; n.hiz[k] = hi[2];
+  }
+}
+
+void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* triLeaf, int firstTri,
+                       int numTris, hipStream_t s) {
+  if (numTris <= 0) return;
+  hipLaunchKernelGGL(k_refit_tris, dim3((numTris + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, tris, indices,
+                     positions, triLeaf, firstTri, numTris);
+}
+
+void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
+                        const int* levelNodes, int count, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(k_refit_nodes, dim3((count + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes, tris,
+                     indices, positions, levelNodes, count);
+}
+
+}  // namespace yrt

@@ -112,6 +112,12 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
 int trace_profile(unsigned long long* out8, int reset);
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s);
+// BVH refit after faceCamera updates: rewrite triangles [firstTri, firstTri+numTris) (global
+// ids) from the vertex buffer, then refit one tree level of nodes (call deepest level first)
+void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* triLeaf, int firstTri,
+                       int numTris, hipStream_t s);
+void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
+                        const int* levelNodes, int count, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 

@@ -332,6 +332,15 @@ class Device:
         N.dev.yrtGetCapturedRays(self.h, int(shadow), depth, org.ctypes.data, dir_.ctypes.data, m, C.byref(tot))
         return org, dir_, tot.value
 
+    def set_refit_commits(self, on=True):
+        self._rc(N.dev.yrtSetRefitCommits(self.h, int(on)), "set_refit_commits")
+
+    def scene_refits(self, scene) -> int:
+        n = N.dev.yrtGetSceneRefits(self.h, scene)
+        if n < 0:
+            raise RuntimeError(f"scene_refits: {self.error()}")
+        return n
+
     def set_tile_shard(self, index, count):
         self._rc(N.dev.yrtSetTileShard(self.h, int(index), int(count)), "set_tile_shard")
 

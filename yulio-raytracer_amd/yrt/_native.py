@@ -142,6 +142,8 @@ _sig(dev, "yrtExportFrame", C.c_int64, vp, vp, vp, vp, vp, sz)
 _sig(dev, "yrtSetFrameSeed", i32, vp, C.c_uint32)
 _sig(dev, "yrtSetBatchCapacity", i32, vp, C.c_int64)
 _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
+_sig(dev, "yrtSetRefitCommits", i32, vp, i32)
+_sig(dev, "yrtGetSceneRefits", i32, vp, vp)
 _sig(dev, "yrtSetRayCapture", i32, vp, i32)
 _sig(dev, "yrtGetCapturedRays", C.c_int64, vp, i32, i32, vp, vp, sz, C.POINTER(C.c_double))
 _sig(dev, "yrtDebugTraceProfile", i32, vp, C.POINTER(C.c_uint64), i32)
