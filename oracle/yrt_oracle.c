@@ -294,7 +294,11 @@ static int p_obj(const Obj* o, const char* n) {
 }
 
 /* ====================================================================== scene objects */
-enum { MT_NONE = 0, MT_MATTE, MT_MATTE_TEX, MT_METALLIC, MT_OBJ, MT_UBER, MT_THIN };
+enum { MT_NONE = 0, MT_MATTE, MT_MATTE_TEX, MT_METALLIC, MT_OBJ, MT_UBER, MT_THIN, MT_PLASTIC, MT_DIELECTRIC,
+       MT_MIRROR, MT_METAL, MT_BRUSHED, MT_VELVET };
+/* materials/medium.h: transmission + refraction index, compared by value */
+typedef struct { V3 T; float eta; } Medium;
+static inline int med_eq(Medium a, Medium b) { return veq(a.T, b.T) && a.eta == b.eta; }
 typedef struct {
   int type;
   V3 reflectance;                               /* Matte */
@@ -306,6 +310,10 @@ typedef struct {
   int map_d, map_Kd, map_Ks, map_Ns, map_Bump;
   V3 diffuse; float roughness, reflectivity, rcpRoughness;  /* Uber */
   V3 transmission; float thickness, transparency;           /* ThinDielectric */
+  V3 pigment;                                               /* Plastic (eta, roughness shared) */
+  Medium outside, inside;                                   /* Dielectric */
+  V3 metalEta, metalK; float roughnessX, roughnessY;        /* Metal / BrushedMetal (reflectance) */
+  float backScattering, fallOff; V3 horizon;                /* Velvet (reflectance) */
 } Material;
 
 enum { GK_FULL = 0, GK_NORMALS = 1, GK_TRIANGLE = 2 };
@@ -320,7 +328,7 @@ typedef struct {
   V3 Ng;
 } Mesh;
 
-enum { LT_AMBIENT = 0, LT_TRIANGLE = 1, LT_HDRI = 2 };
+enum { LT_AMBIENT = 0, LT_TRIANGLE = 1, LT_HDRI = 2, LT_POINT = 3, LT_SPOT = 4, LT_DIRECTIONAL = 5, LT_DISTANT = 6 };
 typedef struct {
   int type;
   V3 L, v0, v1, v2, e1, e2, Ng;
@@ -330,6 +338,8 @@ typedef struct {
   float *ycdf, *ypdf, *xcdf, *xpdf;
   int illumMask, shadowMask;
   int precomp; /* slot or -1 */
+  V3 P, D;     /* point/spot position; spot _D, directional/distant _wo */
+  float cosMin, cosMax, halfAngle, cosHalf;
 } Light;
 
 typedef struct {
@@ -497,6 +507,41 @@ static void mat_build(const Blob* B, int oi, Material* m) {
     m->eta = p_float(o, "eta", 1.4f);
     m->thickness = p_float(o, "thickness", .1f);
     m->transparency = p_float(o, "transparency", 1.f);
+  } else if (!strcasecmp(t, "Plastic")) { /* plastic.h:21-26 */
+    m->type = MT_PLASTIC;
+    m->pigment = p_v3(o, "pigmentColor", vs(1.0f));
+    m->eta = p_float(o, "eta", 1.4f);
+    m->roughness = p_float(o, "roughness", 0.01f);
+    m->rcpRoughness = rcp(m->roughness);
+  } else if (!strcasecmp(t, "Dielectric") || !strcasecmp(t, "Glass")) { /* dielectric.h:13-27 */
+    m->type = MT_DIELECTRIC;
+    m->outside.eta = p_float(o, "etaOutside", 1.0f);
+    m->inside.eta = p_float(o, "etaInside", 1.4f);
+    m->outside.T = p_v3(o, "transmissionOutside", vs(1.0f));
+    m->inside.T = p_v3(o, "transmission", vs(1.0f));
+  } else if (!strcasecmp(t, "Mirror")) { /* mirror.h:15-17 */
+    m->type = MT_MIRROR;
+    m->reflectance = p_v3(o, "reflectance", vs(1.0f));
+  } else if (!strcasecmp(t, "Metal")) { /* metal.h:18-24 */
+    m->type = MT_METAL;
+    m->reflectance = p_v3(o, "reflectance", vs(1.0f));
+    m->metalEta = p_v3(o, "eta", vs(1.4f));
+    m->metalK = p_v3(o, "k", vs(0.0f));
+    m->roughness = p_float(o, "roughness", 0.01f);
+    m->rcpRoughness = rcp(m->roughness);
+  } else if (!strcasecmp(t, "BrushedMetal")) { /* brushedmetal.h:19-27 */
+    m->type = MT_BRUSHED;
+    m->reflectance = p_v3(o, "reflectance", vs(1.0f));
+    m->metalEta = p_v3(o, "eta", vs(1.4f));
+    m->metalK = p_v3(o, "k", vs(0.0f));
+    m->roughnessX = p_float(o, "roughnessX", 0.01f);
+    m->roughnessY = p_float(o, "roughnessY", 0.01f);
+  } else if (!strcasecmp(t, "Velvet")) { /* velvet.h:16-21 */
+    m->type = MT_VELVET;
+    m->reflectance = p_v3(o, "reflectance", vs(1.0f));
+    m->backScattering = p_float(o, "backScattering", 0.0f);
+    m->horizon = p_v3(o, "horizonScatteringColor", vs(1.0f));
+    m->fallOff = p_float(o, "horizonScatteringFallOff", 0.0f);
   } else {
     m->type = MT_NONE;
   }
@@ -679,6 +724,27 @@ static int light_build(const Blob* B, int oi, A3 xfm, int illum, int shadow, Lig
     L->ycdf = d.ycdf; L->ypdf = d.ypdf; L->xcdf = d.xcdf; L->xpdf = d.xpdf;
     L->l2w = aamul(xfm, l2w);
     L->w2l = a3_inv(L->l2w);
+  } else if (!strcasecmp(o->type, "pointlight")) { /* pointlight.h:24-34 */
+    L->type = LT_POINT;
+    L->P = xfmPoint(xfm, p_v3(o, "P", vs(0.f)));
+    L->L = p_v3(o, "I", vs(0.f));
+  } else if (!strcasecmp(o->type, "spotlight")) { /* spotlight.h:24-39 */
+    L->type = LT_SPOT;
+    L->P = xfmPoint(xfm, p_v3(o, "P", vs(0.f)));
+    L->D = xfmVector(xfm, neg(normalize(p_v3(o, "D", vs(0.f)))));
+    L->L = p_v3(o, "I", vs(0.f));
+    L->cosMin = cosf(0.5f * deg2rad(p_float(o, "angleMin", 0.f)));
+    L->cosMax = cosf(0.5f * deg2rad(p_float(o, "angleMax", 0.f)));
+  } else if (!strcasecmp(o->type, "directionallight")) { /* directionallight.h:13-29 */
+    L->type = LT_DIRECTIONAL;
+    L->D = normalize(xfmVector(xfm, neg(normalize(p_v3(o, "D", vs(0.f))))));
+    L->L = p_v3(o, "E", vs(0.f));
+  } else if (!strcasecmp(o->type, "distantlight")) { /* distantlight.h:16-36 */
+    L->type = LT_DISTANT;
+    L->D = normalize(xfmVector(xfm, neg(normalize(p_v3(o, "D", vs(0.f))))));
+    L->L = p_v3(o, "L", vs(0.f));
+    L->halfAngle = deg2rad(p_float(o, "halfAngle", 0.f));
+    L->cosHalf = cosf(L->halfAngle);
   } else {
     return -1;
   }
@@ -856,7 +922,8 @@ static int world_build(const Blob* B, World* W) {
         free(primLight); free(primShape);
         return fail("light type outside the oracle's scope");
       }
-      if (L->type == LT_AMBIENT || L->type == LT_HDRI) W->env[W->nenv++] = W->nlights;
+      /* EnvironmentLight subclasses (api/scene.h:76) */
+      if (L->type == LT_AMBIENT || L->type == LT_HDRI || L->type == LT_DISTANT) W->env[W->nenv++] = W->nlights;
       if (L->type == LT_HDRI) L->precomp = npre++;
       primLight[i] = W->nlights++;
       primShape[i] = shape;
@@ -1298,13 +1365,15 @@ static void post_intersect(const World* W, const Ray* r, const Hit* h, DG* dg) {
 
 /* ---- BRDF components (brdfs/ headers); type bits brdfs/brdf.h:10-30 */
 #define BT_DIFFUSE 0x000F000Fu
-enum { B_LAMBERT, B_DIEL_REFL, B_CONST_TRANS, B_THIN_TRANS, B_LAYER, B_MICRO, B_TRANS, B_SPEC };
-typedef struct { int kind; uint32_t type; V3 R; float a, b, c; } Brdf;
+enum { B_LAMBERT, B_DIEL_REFL, B_CONST_TRANS, B_THIN_TRANS, B_LAYER, B_MICRO, B_TRANS, B_SPEC, B_REFL, B_COND,
+       B_MICRO_COND, B_MICRO_ANISO, B_MINNAERT, B_VELVETY, B_DIEL_TRANS };
+typedef struct { int kind; uint32_t type; V3 R; float a, b, c; V3 eta, k; } Brdf;
 typedef struct { int n; Brdf c[8]; } BSet;
 static void bs_add(BSet* s, int kind, uint32_t type, V3 R, float a, float b, float c) {
   if (s->n >= 8) return;
   Brdf* k = &s->c[s->n++];
   k->kind = kind; k->type = type; k->R = R; k->a = a; k->b = b; k->c = c;
+  k->eta = k->k = vs(0.f);
 }
 
 /* optics.h:64-104 */
@@ -1340,7 +1409,28 @@ static V3 cos_hemi(float u, float v, V3 N, float* pdf) {
 
 static V3 lambert_eval(V3 R, const DG* dg, V3 wi) { return muls(muls(R, ONE_OVER_PI_F), clamp01(dot(wi, dg->Ns))); }
 
-/* Microfacet<FresnelDielectric,PowerCosineDistribution>::eval (brdfs/microfacet.h:28-41) */
+/* fresnelConductor (brdfs/optics.h:123-131), per channel */
+static float fres_cond1(float cosi, float eta, float k) {
+  const float tmp = eta * eta + k * k;
+  const float e2c = 2.0f * eta * cosi;
+  const float Rpar = (tmp * cosi * cosi - e2c + 1.0f) * rcp(tmp * cosi * cosi + e2c + 1.0f);
+  const float Rper = (tmp - e2c + cosi * cosi) * rcp(tmp + e2c + cosi * cosi);
+  return 0.5f * (Rpar + Rper);
+}
+static V3 fres_cond(float cosi, V3 eta, V3 k) {
+  return v3(fres_cond1(cosi, eta.x, k.x), fres_cond1(cosi, eta.y, k.y), fres_cond1(cosi, eta.z, k.z));
+}
+/* AnisotropicPowerCosineDistribution::eval (microfacet/anisotropic_power_cosine_distribution.h:40-48) */
+static float aniso_D(float nx, float ny, const DG* dg, V3 wh) {
+  const float norm2 = sqrtf((nx + 2) * (ny + 2)) * ONE_OVER_TWO_PI_F;
+  const float cP = dot(wh, dg->Tx), sP = dot(wh, dg->Ty), cT = dot(wh, dg->Ns);
+  const float R = cP * cP + sP * sP;
+  if (R == 0.0f) return norm2;
+  const float n = (nx * (cP * cP) + ny * (sP * sP)) * rcp(R);
+  return norm2 * powf(fabsf(cT), n);
+}
+/* Microfacet<Fresnel,Distribution>::eval (brdfs/microfacet.h:28-41): dielectric or conductor
+ * Fresnel, power-cosine or anisotropic power-cosine distribution */
 static V3 micro_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   if (dot(wi, dg->Ng) <= 0) return vs(0.f);
   const float cO = dot(wo, dg->Ns), cI = dot(wi, dg->Ns);
@@ -1348,11 +1438,29 @@ static V3 micro_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const V3 wh = normalize(add(wi, wo));
   const float cH = dot(wh, dg->Ns);
   const float cT = dot(wi, wh);
-  const float F = fres2(cT, c->a * rcp(c->b), NULL);
-  const float n = c->c;
-  const float D = ((n + 2) * ONE_OVER_TWO_PI_F) * powf(fabsf(dot(wh, dg->Ns)), n);
+  const V3 F = c->kind == B_MICRO ? vs(fres2(cT, c->a * rcp(c->b), NULL)) : fres_cond(cT, c->eta, c->k);
+  float D;
+  if (c->kind == B_MICRO_ANISO) {
+    D = aniso_D(c->a, c->b, dg, wh);
+  } else {
+    const float n = c->kind == B_MICRO ? c->c : c->a;
+    D = ((n + 2) * ONE_OVER_TWO_PI_F) * powf(fabsf(dot(wh, dg->Ns)), n);
+  }
   const float G = fminf(fminf(1.0f, 2.0f * cH * cO * rcp(cT)), 2.0f * cH * cI * rcp(cT));
-  return muls(mulv(muls(muls(c->R, D), G), vs(F)), rcp(4.0f * cO));
+  return muls(mulv(muls(muls(c->R, D), G), F), rcp(4.0f * cO));
+}
+/* Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26) */
+static V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+static V3 minnaert_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
+  const float cI = clamp01(dot(wi, dg->Ns));
+  const float bs = powf(clamp01(dot(wo, wi)), c->a);
+  return divs(muls(muls(c->R, bs), cI), PI_F);
+}
+static V3 velvety_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
+  const float cO = clamp01(dot(wo, dg->Ns)), cI = clamp01(dot(wi, dg->Ns));
+  const float sO = sqrtf(1.0f - cO * cO);
+  const float hs = powf(sO, c->a);
+  return divs(muls(muls(c->R, hs), cI), PI_F);
 }
 /* DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38) */
 static V3 layer_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
@@ -1377,8 +1485,11 @@ static V3 brdf_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   switch (c->kind) {
     case B_LAMBERT: return lambert_eval(c->R, dg, wi);
     case B_LAYER: return layer_eval(c, wo, dg, wi);
-    case B_MICRO: return micro_eval(c, wo, dg, wi);
+    case B_MICRO: case B_MICRO_COND: case B_MICRO_ANISO: return micro_eval(c, wo, dg, wi);
     case B_SPEC: return spec_eval(c, wo, dg, wi);
+    case B_REFL: return c->R;
+    case B_MINNAERT: return minnaert_eval(c, wo, dg, wi);
+    case B_VELVETY: return velvety_eval(c, wo, dg, wi);
     default: return vs(0.f);
   }
 }
@@ -1451,6 +1562,61 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       *wi = neg(wo);
       *pdf = 1.0f;
       return c->R;
+    case B_MICRO_COND: { /* microfacet.h:43-50 + power_cosine_distribution.h:27-35 */
+      if (dot(wo, dg->Ns) <= 0.0f) return vs(0.f);
+      const float n = c->a;
+      const float norm1 = (n + 1) * ONE_OVER_TWO_PI_F;
+      const float phi = TWO_PI_F * sx;
+      const float cP = cosf(phi), sP = sinf(phi);
+      const float cT = powf(sy, rcp(n + 1));
+      const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
+      const V3 wh = lmul(frame_(dg->Ns), v3(cP * sT, sP * sT, cT));
+      const float whpdf = norm1 * powf(cT, n);
+      *wi = reflect2(wo, wh);
+      *pdf = whpdf * rcp(4.0f * fabsf(dot(wo, wh)));
+      if (dot(*wi, dg->Ns) <= 0.0f) return vs(0.f);
+      return micro_eval(c, wo, dg, *wi);
+    }
+    case B_MICRO_ANISO: { /* anisotropic_power_cosine_distribution.h:57-73 */
+      if (dot(wo, dg->Ns) <= 0.0f) return vs(0.f);
+      const float nx = c->a, ny = c->b;
+      const float norm1 = sqrtf((nx + 1) * (ny + 1)) * ONE_OVER_TWO_PI_F;
+      const float phi = TWO_PI_F * sx;
+      const float sP0 = sqrtf(nx + 1) * sinf(phi);
+      const float cP0 = sqrtf(ny + 1) * cosf(phi);
+      const float nrm = rsqrt_(sP0 * sP0 + cP0 * cP0);
+      const float sP = sP0 * nrm, cP = cP0 * nrm;
+      const float n = nx * (cP * cP) + ny * (sP * sP);
+      const float cT = powf(sy, rcp(n + 1));
+      const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
+      const float whpdf = norm1 * powf(cT, n);
+      const V3 h = v3(cP * sT, sP * sT, cT);
+      const V3 wh = add(add(muls(dg->Tx, h.x), muls(dg->Ty, h.y)), muls(dg->Ns, h.z));
+      *wi = reflect2(wo, wh);
+      *pdf = whpdf * rcp(4.0f * fabsf(dot(wo, wh)));
+      if (dot(*wi, dg->Ns) <= 0.0f) return vs(0.f);
+      return micro_eval(c, wo, dg, *wi);
+    }
+    case B_REFL: /* reflection.h:19-22 */
+      *wi = reflect2(wo, dg->Ns);
+      *pdf = 1.0f;
+      return c->R;
+    case B_COND: /* conductor.h:21-24 */
+      *wi = reflect2(wo, dg->Ns);
+      *pdf = 1.0f;
+      return mulv(c->R, fres_cond(dot(wo, dg->Ns), c->eta, c->k));
+    case B_MINNAERT:
+      *wi = cos_hemi(sx, sy, dg->Ns, pdf);
+      return minnaert_eval(c, wo, dg, *wi);
+    case B_VELVETY:
+      *wi = cos_hemi(sx, sy, dg->Ns, pdf);
+      return velvety_eval(c, wo, dg, *wi);
+    case B_DIEL_TRANS: { /* dielectric.h:82-89 */
+      const float cO = clamp01(dot(wo, dg->Ns));
+      float cI;
+      *pdf = refract5(wo, dg->Ns, c->a, cO, &cI, wi);
+      return vs(1.0f - fres3(cO, cI, c->a));
+    }
     case B_SPEC: { /* specular.h:26-28, shapesampler.h:104-121 */
       const float e = c->a;
       const float phi = TWO_PI_F * sx;
@@ -1502,11 +1668,40 @@ static V3 bs_sample(const BSet* s, V3 wo, const DG* dg, float sx, float sy, floa
 }
 
 /* Material::shade (materials/ headers) */
-static void shade(const World* W, const Material* m, DG* dg, BSet* s) {
+static void shade(const World* W, const Material* m, Medium cur, DG* dg, BSet* s) {
   const Blob* B = W->blob;
   s->n = 0;
   float c[4];
   switch (m->type) {
+    case MT_PLASTIC: /* DielectricLayer<Lambertian>(one, 1, eta, pigment) + DielectricReflection(1, eta) | Microfacet */
+      bs_add(s, B_LAYER, 0x1u, m->pigment, 1.0f * rcp(m->eta), m->eta * rcp(1.0f), 0);
+      if (m->roughness == 0.0f) bs_add(s, B_DIEL_REFL, 0x100u, vs(0.f), 1.0f * rcp(m->eta), 1.0f, 0);
+      else bs_add(s, B_MICRO, 0x10u, vs(1.0f), 1.0f, m->eta, m->rcpRoughness);
+      break;
+    case MT_DIELECTRIC: { /* dielectric.h:42-52 */
+      const int oi = med_eq(cur, m->outside);
+      const float e = oi ? m->outside.eta * rcp(m->inside.eta) : m->inside.eta * rcp(m->outside.eta);
+      bs_add(s, B_DIEL_REFL, 0x100u, vs(0.f), e, 1.0f, 0);
+      bs_add(s, B_DIEL_TRANS, 0x01000000u, vs(0.f), e, 0, 0);
+      break;
+    }
+    case MT_MIRROR: bs_add(s, B_REFL, 0x100u, m->reflectance, 0, 0, 0); break;
+    case MT_METAL:
+      if (m->roughness == 0.0f) bs_add(s, B_COND, 0x100u, m->reflectance, 0, 0, 0);
+      else bs_add(s, B_MICRO_COND, 0x10u, m->reflectance, m->rcpRoughness, 0, 0);
+      s->c[s->n - 1].eta = m->metalEta;
+      s->c[s->n - 1].k = m->metalK;
+      break;
+    case MT_BRUSHED:
+      if (m->roughnessX == 0.0f || m->roughnessY == 0.0f) bs_add(s, B_COND, 0x100u, m->reflectance, 0, 0, 0);
+      else bs_add(s, B_MICRO_ANISO, 0x10u, m->reflectance, rcp(m->roughnessX), rcp(m->roughnessY), 0);
+      s->c[s->n - 1].eta = m->metalEta;
+      s->c[s->n - 1].k = m->metalK;
+      break;
+    case MT_VELVET:
+      bs_add(s, B_MINNAERT, 0x1u, m->reflectance, m->backScattering, 0, 0);
+      bs_add(s, B_VELVETY, 0x1u, m->horizon, m->fallOff, 0, 0);
+      break;
     case MT_MATTE: bs_add(s, B_LAMBERT, 0x1u, m->reflectance, 0, 0, 0); break;
     case MT_MATTE_TEX:
       if (m->Kd >= 0) {
@@ -1625,6 +1820,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
 #define S2Y(d) T->t[(size_t)(5 + T->n1 + 2 * (d) + 1) * T->rec + rec]
   V3 L = vs(0.f), thr = vs(1.f);
   int depth = 0, ignoreVL = 0;
+  Medium medium = {vs(1.0f), 1.0f}; /* Medium::Vacuum() */
   const float eta = 1.f; /* Sample copy drops eta */
   while (depth < R->maxDepth) {
     if (fmax3(thr) < R->minContribution) break;
@@ -1635,7 +1831,11 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
       if (!ignoreVL)
         for (int i = 0; i < W->nenv; i++) {
           const Light* E = &W->lights[W->env[i]];
-          L = add(L, mulv(thr, E->type == LT_AMBIENT ? E->L : hdri_Le(W, E, wo)));
+          V3 Le;
+          if (E->type == LT_AMBIENT) Le = E->L;
+          else if (E->type == LT_DISTANT) Le = dot(neg(wo), E->D) >= E->cosHalf ? E->L : vs(0.f); /* distantlight.h:38-41 */
+          else Le = hdri_Le(W, E, wo);
+          L = add(L, mulv(thr, Le));
         }
       break;
     }
@@ -1645,7 +1845,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     if (dot(dg.Ng, ray.dir) > 0.f) { backfacing = 1; dg.Ng = neg(dg.Ng); dg.Ns = neg(dg.Ns); }
     BSet bs;
     bs.n = 0;
-    shade(W, &W->mats[dg.material], &dg, &bs);
+    shade(W, &W->mats[dg.material], medium, &dg, &bs);
     if (!ignoreVL && dg.light >= 0 && !backfacing) L = add(L, mulv(thr, W->lights[dg.light].L));
     int useDirect = 0;
     for (int i = 0; i < bs.n; i++) useDirect |= (bs.c[i].type & BT_DIFFUSE) != 0;
@@ -1673,6 +1873,32 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
           wi = muls(d, rcp(tMax));
           pdf = 2.0f * tMax * tMax * tMax * rcp(fabsf(dDotNg));
           Ls = Lt->L;
+        } else if (Lt->type == LT_POINT) { /* pointlight.h:36-42 */
+          const V3 d = sub(Lt->P, dg.P);
+          const float dist = length(d);
+          wi = divs(d, dist);
+          pdf = dist * dist;
+          Ls = Lt->L;
+        } else if (Lt->type == LT_SPOT) { /* spotlight.h:41-52 */
+          const V3 d = sub(Lt->P, dg.P);
+          const float dist = length(d);
+          wi = muls(d, rcp(dist));
+          pdf = dist * dist;
+          const float ca = dot(wi, Lt->D);
+          if (Lt->cosMin != Lt->cosMax) Ls = muls(Lt->L, clamp01((ca - Lt->cosMax) * rcp(Lt->cosMin - Lt->cosMax)));
+          else Ls = ca > Lt->cosMin ? Lt->L : vs(0.f);
+        } else if (Lt->type == LT_DIRECTIONAL) { /* directionallight.h:31-33 */
+          wi = Lt->D;
+          pdf = 1.0f;
+          Ls = Lt->L;
+        } else if (Lt->type == LT_DISTANT) { /* distantlight.h:46-50, shapesampler.h:149-165 */
+          const float ang = Lt->halfAngle;
+          const float phi = TWO_PI_F * S2X(0);
+          const float cT = 1.0f - S2Y(0) * (1.0f - cosf(ang));
+          const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
+          pdf = rcp(4.0f * PI_F * (sinf(0.5f * ang) * sinf(0.5f * ang)));
+          wi = lmul(frame_(Lt->D), v3(cosf(phi) * sT, sinf(phi) * sT, cT));
+          Ls = Lt->L;
         }
         if (v3zero(Ls) || pdf == 0.f) continue;
         const V3 brdf = bs_eval(&bs, wo, &dg, wi, BT_DIFFUSE);
@@ -1697,8 +1923,15 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     V3 wi;
     float pdf;
     uint32_t type;
-    const V3 c = bs_sample(&bs, wo, &dg, S2X(1 + depth), S2Y(1 + depth), S1(depth), &wi, &pdf, &type);
+    V3 c = bs_sample(&bs, wo, &dg, S2X(1 + depth), S2Y(1 + depth), S1(depth), &wi, &pdf, &type);
     if (v3zero(c) || pdf <= 0.f) break;
+    /* simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207) */
+    if (!veq(medium.T, vs(1.0f)))
+      c = mulv(c, v3(powf(medium.T.x, h.t), powf(medium.T.y, h.t), powf(medium.T.z, h.t)));
+    if (type & 0xFFFF0000u) {
+      const Material* mt = &W->mats[dg.material];
+      if (mt->type == MT_DIELECTRIC) medium = med_eq(medium, mt->inside) ? mt->outside : mt->inside;
+    }
     thr = muls(mulv(thr, c), rcp(pdf));
     ignoreVL = (type & BT_DIFFUSE) != 0;
     ray.org = dg.P;

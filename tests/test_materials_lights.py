@@ -1,0 +1,64 @@
+"""the reference materials and lights outside the BASELINE configs —
+Plastic, Dielectric (with medium tracking and the volumetric transmission term), Mirror,
+Metal, BrushedMetal, Velvet (devices/device_singleray/materials/*.h) and point, spot,
+directional, distant lights (lights/*.h) — through the XML loader and the command-line tags
+(scenes/materials_lights.{xml,ecs}, written by tools/make_materials_scene.py), GPU against
+the oracle restatement on the same frame."""
+import numpy as np
+import pytest
+
+import dae_scene
+import oracle
+import yrt
+from helpers import SCENES, parity
+
+ARGS = ["-c", str(SCENES / "materials_lights.ecs")]
+
+
+def test_scene_objects_and_defaults(host_device):
+    s = yrt.Session(ARGS + ["-size", "32", "32"], device=host_device)
+    objs = dae_scene.blob_objects(s.export_frame())
+    mats = sorted({o[1] for o in objs if o[0] == "MATERIAL"})
+    lights = sorted({o[1] for o in objs if o[0] == "LIGHT"})
+    assert mats == ["BrushedMetal", "Dielectric", "Matte", "Metal", "Mirror", "Plastic", "Velvet"]
+    assert lights == ["ambientlight", "directionallight", "distantlight", "pointlight", "spotlight"]
+    spot = [o[2] for o in objs if o[1] == "spotlight"][0]
+    assert spot["D"][:3] == pytest.approx((0.0, -1.0, 0.0))  # AffineSpace column vz (xml_loader.cpp:293)
+    assert spot["angleMin"][0] == 35 and spot["angleMax"][0] == 55
+    s.close()
+
+
+def test_masked_pointlight_tag(host_device):
+    s = yrt.Session(ARGS + ["-size", "16", "16", "-masked_pointlight", "1", "2", "3", "10", "10", "10", "2", "5"],
+                    device=host_device)
+    assert oracle.render(s.export_frame(), 16, 16, 1.0)[0].mean() > 0
+    s.close()
+
+
+def test_oracle_render(host_device):
+    s = yrt.Session(ARGS + ["-size", "24", "18", "-spp", "2"], device=host_device)
+    img, st = oracle.render(s.export_frame(), 24, 18, 1.0)
+    assert np.isfinite(img).all() and img.mean() > 0.02
+    assert st["raysShadow"] > st["raysClosest"]  # five lights per diffuse vertex
+    s.close()
+
+
+def test_unknown_types_raise(host_device):
+    with pytest.raises(RuntimeError, match="unknown material type"):
+        host_device.rtNewMaterial("Chrome")
+    with pytest.raises(RuntimeError, match="unknown light type"):
+        host_device.rtNewLight("arealight")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [2, 6])
+def test_materials_lights_parity(gpu_device, depth):
+    """GPU vs oracle, RGB_FLOAT32: every new BRDF component (reflection, conductor, rough and
+    anisotropic conductor microfacets, Minnaert, Velvety, dielectric transmission through two
+    interfaces with the in-medium attenuation) and every light sampler."""
+    s = yrt.Session(ARGS + ["-size", "96", "72", "-spp", "8", "-depth", str(depth), "-fb", "RGB_FLOAT32"],
+                    device=gpu_device)
+    img = s.render()
+    ref, _ = oracle.render(s.export_frame(), 96, 72, s.info()["gamma"])
+    parity(img, ref, 0.995, mad_rel=2e-4)
+    s.close()

@@ -53,6 +53,12 @@ enum MaterialType : int32_t {
   MAT_OBJ = 4,
   MAT_UBER = 5,
   MAT_THIN_DIELECTRIC = 6,
+  MAT_PLASTIC = 7,
+  MAT_DIELECTRIC = 8,
+  MAT_MIRROR = 9,
+  MAT_METAL = 10,
+  MAT_BRUSHED_METAL = 11,
+  MAT_VELVET = 12,
 };
 
 // Parameter slots per material type (filled by device/materials.cpp from Parms with the
@@ -61,7 +67,7 @@ struct GpuMaterial {
   int32_t type;
   int32_t tex[5];   // texture ids (-1 none). Uber/MatteTextured/ThinDielectric: tex[0]=Kd.
                     // Obj: map_d, map_Kd, map_Ks, map_Ns, map_Bump
-  int32_t pad[2];
+  int32_t media[2];  // Dielectric: medium table indices (outside, inside); other types unused
   float p[24];
 };
 
@@ -77,7 +83,15 @@ struct GpuTexture {
   int32_t image, filter, invert, pad;
 };
 
-enum LightType : int32_t { LIGHT_AMBIENT = 0, LIGHT_TRIANGLE = 1, LIGHT_HDRI = 2 };
+enum LightType : int32_t {
+  LIGHT_AMBIENT = 0,
+  LIGHT_TRIANGLE = 1,
+  LIGHT_HDRI = 2,
+  LIGHT_POINT = 3,        // v0 = P, L = I
+  LIGHT_SPOT = 4,         // v0 = P, e1 = _D (negative direction), L = I, bsphere = (cosMin, cosMax)
+  LIGHT_DIRECTIONAL = 5,  // e1 = _wo, L = E
+  LIGHT_DISTANT = 6,      // e1 = _wo, L, bsphere = (halfAngle, cosHalfAngle); also an env light
+};
 struct GpuLight {
   int32_t type, illumMask, shadowMask, precomputed;  // precomputed: index into light-sample slots or -1
   int32_t isEnv, image, distOffset, pad;             // HDRI: image id, distribution offset (floats)

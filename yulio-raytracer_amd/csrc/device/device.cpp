@@ -533,12 +533,12 @@ YRTHandle yrtNewTexture(YRTDevice dev, const char* type) {
 
 YRTHandle yrtNewMaterial(YRTDevice dev, const char* type) {
   DEV_GUARD(dev, nullptr)
-  static const char* ok[] = {"Matte", "MatteTextured", "MetallicPaint", "Obj", "Uber", "ThinDielectric", "ThinGlass"};
+  // SingleRayDevice::rtNewMaterial (api/singleray_device.cpp:262-280)
+  static const char* ok[] = {"Matte", "Plastic", "Dielectric", "Glass", "ThinDielectric", "ThinGlass", "Mirror",
+                             "Metal", "BrushedMetal", "MetallicPaint", "MatteTextured", "Uber", "Obj", "Velvet"};
   bool found = false;
   for (auto* n : ok) found |= ieq(type, n);
-  if (!found)
-    throw std::runtime_error(std::string("material type '") + type +
-                             "' is outside the MI355X device's scope (SURVEY.md §2 row 11)");
+  if (!found) throw std::runtime_error(std::string("unknown material type: ") + type);
   return dev->d->wrap(std::make_shared<MaterialObj>(type));
   DEV_END(nullptr)
 }
@@ -553,9 +553,12 @@ YRTHandle yrtNewShape(YRTDevice dev, const char* type) {
 
 YRTHandle yrtNewLight(YRTDevice dev, const char* type) {
   DEV_GUARD(dev, nullptr)
-  if (!ieq(type, "ambientlight") && !ieq(type, "trianglelight") && !ieq(type, "hdrilight"))
-    throw std::runtime_error(std::string("light type '") + type +
-                             "' is outside the MI355X device's scope (SURVEY.md §2 row 13)");
+  // SingleRayDevice::rtNewLight (api/singleray_device.cpp:293-302)
+  static const char* ok[] = {"ambientlight", "pointlight", "spotlight", "directionallight", "distantlight",
+                             "hdrilight", "trianglelight"};
+  bool found = false;
+  for (auto* n : ok) found |= ieq(type, n);
+  if (!found) throw std::runtime_error(std::string("unknown light type: ") + type);
   return dev->d->wrap(std::make_shared<LightObj>(type));
   DEV_END(nullptr)
 }

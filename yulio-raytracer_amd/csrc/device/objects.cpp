@@ -135,9 +135,63 @@ void MaterialObj::commit() {
     p[8] = parms.getFloat("thickness", .1f);
     p[9] = parms.getFloat("transparency", 1.f);
     p[10] = 1.0f * rcpf_(eta);
+  } else if (ieq(type, "Plastic")) {
+    // materials/plastic.h:21-26
+    m->gm.type = MAT_PLASTIC;
+    V3 pc = parms.getV3("pigmentColor", v3s(1.f));
+    float eta = parms.getFloat("eta", 1.4f);
+    float roughness = parms.getFloat("roughness", 0.01f);
+    p[0] = pc.x; p[1] = pc.y; p[2] = pc.z;
+    p[3] = eta;
+    p[4] = roughness;
+    p[5] = rcpf_(roughness);
+    p[6] = 1.0f * rcpf_(eta);   // DielectricLayer(one, 1, eta): etait
+    p[7] = eta * rcpf_(1.0f);   // etati
+    p[8] = 1.0f * rcpf_(eta);   // DielectricReflection(1, eta): eta_
+  } else if (ieq(type, "Dielectric") || ieq(type, "Glass")) {
+    // materials/dielectric.h:13-27: media interface; components picked per current medium
+    m->gm.type = MAT_DIELECTRIC;
+    const float etaOut = parms.getFloat("etaOutside", 1.0f), etaIn = parms.getFloat("etaInside", 1.4f);
+    const V3 tOut = parms.getV3("transmissionOutside", v3s(1.f)), tIn = parms.getV3("transmission", v3s(1.f));
+    p[0] = tOut.x; p[1] = tOut.y; p[2] = tOut.z; p[3] = etaOut;
+    p[4] = tIn.x; p[5] = tIn.y; p[6] = tIn.z; p[7] = etaIn;
+    p[8] = etaOut * rcpf_(etaIn);  // *_oi: DielectricReflection/Transmission(etaOutside, etaInside)
+    p[9] = etaIn * rcpf_(etaOut);  // *_io
+  } else if (ieq(type, "Mirror")) {
+    // materials/mirror.h:15-17
+    m->gm.type = MAT_MIRROR;
+    V3 r = parms.getV3("reflectance", v3s(1.f));
+    p[0] = r.x; p[1] = r.y; p[2] = r.z;
+  } else if (ieq(type, "Metal")) {
+    // materials/metal.h:18-24
+    m->gm.type = MAT_METAL;
+    V3 r = parms.getV3("reflectance", v3s(1.f)), eta = parms.getV3("eta", v3s(1.4f)), k = parms.getV3("k", v3s(0.f));
+    float roughness = parms.getFloat("roughness", 0.01f);
+    p[0] = r.x; p[1] = r.y; p[2] = r.z;
+    p[3] = eta.x; p[4] = eta.y; p[5] = eta.z;
+    p[6] = k.x; p[7] = k.y; p[8] = k.z;
+    p[9] = roughness;
+    p[10] = rcpf_(roughness);
+  } else if (ieq(type, "BrushedMetal")) {
+    // materials/brushedmetal.h:19-27
+    m->gm.type = MAT_BRUSHED_METAL;
+    V3 r = parms.getV3("reflectance", v3s(1.f)), eta = parms.getV3("eta", v3s(1.4f)), k = parms.getV3("k", v3s(0.f));
+    float rx = parms.getFloat("roughnessX", 0.01f), ry = parms.getFloat("roughnessY", 0.01f);
+    p[0] = r.x; p[1] = r.y; p[2] = r.z;
+    p[3] = eta.x; p[4] = eta.y; p[5] = eta.z;
+    p[6] = k.x; p[7] = k.y; p[8] = k.z;
+    p[9] = rx; p[10] = ry;
+    p[11] = rcpf_(rx); p[12] = rcpf_(ry);
+  } else if (ieq(type, "Velvet")) {
+    // materials/velvet.h:16-21
+    m->gm.type = MAT_VELVET;
+    V3 r = parms.getV3("reflectance", v3s(1.f)), h = parms.getV3("horizonScatteringColor", v3s(1.f));
+    p[0] = r.x; p[1] = r.y; p[2] = r.z;
+    p[3] = parms.getFloat("backScattering", 0.f);
+    p[4] = h.x; p[5] = h.y; p[6] = h.z;
+    p[7] = parms.getFloat("horizonScatteringFallOff", 0.f);
   } else {
-    throw std::runtime_error("material type '" + type +
-                             "' is outside the MI355X device's scope (SURVEY.md §2 row 11)");
+    throw std::runtime_error("unknown material type: " + type);
   }
   inst = m;
 }
@@ -288,6 +342,13 @@ std::shared_ptr<const LightInst> LightInst::transform(const A3& xfm, int illum, 
     // HDRILight::transform: xfm*local2world, world2local = rcp(local2world)
     l->l2w = mul(xfm, l2w);
     l->w2l = a3_inverse(l->l2w);
+  } else if (type == LIGHT_POINT) {
+    l->v0 = xfmPoint(xfm, v0);  // pointlight.h:30-34
+  } else if (type == LIGHT_SPOT) {
+    l->v0 = xfmPoint(xfm, v0);  // spotlight.h:33-39 (direction not renormalized)
+    l->e1 = xfmVector(xfm, e1);
+  } else if (type == LIGHT_DIRECTIONAL || type == LIGHT_DISTANT) {
+    l->e1 = normalize(xfmVector(xfm, e1));  // the private ctors normalize _wo
   }
   return l;
 }
@@ -333,8 +394,33 @@ void LightObj::commit() {
         importance[(size_t)y * w + x] = sinf(kPi * (y + 0.5f) * rcpf_(float(h))) * (c[0] + c[1] + c[2]);
       }
     dist2d_init(importance.data(), w, h, l->ycdf, l->ypdf, l->xcdf, l->xpdf);
+  } else if (ieq(type, "pointlight")) {
+    // lights/pointlight.h:24-27
+    l->type = LIGHT_POINT;
+    l->v0 = parms.getV3("P", v3s(0.f));
+    l->L = parms.getV3("I", v3s(0.f));
+  } else if (ieq(type, "spotlight")) {
+    // lights/spotlight.h:24-31
+    l->type = LIGHT_SPOT;
+    l->v0 = parms.getV3("P", v3s(0.f));
+    l->e1 = -normalize(parms.getV3("D", v3s(0.f)));
+    l->L = parms.getV3("I", v3s(0.f));
+    l->cosAngleMin = cosf(0.5f * deg2rad(parms.getFloat("angleMin", 0.f)));
+    l->cosAngleMax = cosf(0.5f * deg2rad(parms.getFloat("angleMax", 0.f)));
+  } else if (ieq(type, "directionallight")) {
+    // lights/directionallight.h:22-25
+    l->type = LIGHT_DIRECTIONAL;
+    l->e1 = -normalize(parms.getV3("D", v3s(0.f)));
+    l->L = parms.getV3("E", v3s(0.f));
+  } else if (ieq(type, "distantlight")) {
+    // lights/distantlight.h:25-30
+    l->type = LIGHT_DISTANT;
+    l->e1 = -normalize(parms.getV3("D", v3s(0.f)));
+    l->L = parms.getV3("L", v3s(0.f));
+    l->halfAngle = deg2rad(parms.getFloat("halfAngle", 0.f));
+    l->cosHalfAngle = cosf(l->halfAngle);
   } else {
-    throw std::runtime_error("light type '" + type + "' is outside the MI355X device's scope (SURVEY.md §2 row 13)");
+    throw std::runtime_error("unknown light type: " + type);
   }
   inst = l;
 }

@@ -106,6 +106,8 @@ struct LightInst {
   // HDRI importance distribution (lights/hdrilight.cpp:35-40): yCDF/yPDF + per-row x CDF/PDF
   std::vector<float> ycdf, ypdf, xcdf, xpdf;
   int illumMask = -1, shadowMask = -1;
+  float cosAngleMin = 1.f, cosAngleMax = 1.f;   // spot (spotlight.h:29-30)
+  float halfAngle = 0.f, cosHalfAngle = 1.f;    // distant (distantlight.h:28-29)
   std::shared_ptr<const MeshInst> shape;  // TriangleLight::shape()
   std::shared_ptr<const LightInst> transform(const A3& xfm, int illumMask, int shadowMask) const;
   bool precompute() const { return type == LIGHT_HDRI; }

@@ -66,12 +66,25 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     textures.push_back(g);
     return texIds[t.get()] = (int)textures.size() - 1;
   };
+  // medium table (materials/medium.h): [0] = vacuum; Medium::operator== compares by value, so
+  // media are deduplicated by value and compared by index on the GPU
+  std::vector<float4> media = {make_float4(1.f, 1.f, 1.f, 1.f)};
+  auto mediumId = [&](float tr, float tg, float tb, float eta) -> int {
+    for (size_t i = 0; i < media.size(); ++i)
+      if (media[i].x == tr && media[i].y == tg && media[i].z == tb && media[i].w == eta) return (int)i;
+    media.push_back(make_float4(tr, tg, tb, eta));
+    return (int)media.size() - 1;
+  };
   auto materialId = [&](const std::shared_ptr<const MaterialInst>& m) -> int {
     if (!m) return -1;
     auto it = matIds.find(m.get());
     if (it != matIds.end()) return it->second;
     GpuMaterial g = m->gm;
     for (int k = 0; k < 5; ++k) g.tex[k] = textureId(m->tex[k]);
+    if (g.type == MAT_DIELECTRIC) {
+      g.media[0] = mediumId(g.p[0], g.p[1], g.p[2], g.p[3]);  // outside
+      g.media[1] = mediumId(g.p[4], g.p[5], g.p[6], g.p[7]);  // inside
+    }
     materials.push_back(g);
     return matIds[m.get()] = (int)materials.size() - 1;
   };
@@ -100,7 +113,10 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     };
     stA(g.l2w, L.l2w);
     stA(g.w2l, L.w2l);
-    if (L.type == LIGHT_AMBIENT || L.type == LIGHT_HDRI) {
+    g.bsphere[0] = L.type == LIGHT_SPOT ? L.cosAngleMin : L.halfAngle;
+    g.bsphere[1] = L.type == LIGHT_SPOT ? L.cosAngleMax : L.cosHalfAngle;
+    // EnvironmentLight subclasses (api/scene.h:76): ambient, HDRI, distant
+    if (L.type == LIGHT_AMBIENT || L.type == LIGHT_HDRI || L.type == LIGHT_DISTANT) {
       g.isEnv = 1;
       envLights.push_back((int)lights.size());
     }
@@ -213,6 +229,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->texels.upload(texels);
   S->lights.upload(lights);
   S->envLights.upload(envLights);
+  S->media.upload(media);
 
   SceneView& v = S->view;
   v.nodes = S->nodes.as<GpuNode>();
@@ -229,6 +246,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   v.texels = S->texels.as<uint8_t>();
   v.lights = S->lights.as<GpuLight>();
   v.envLights = S->envLights.as<int>();
+  v.media = S->media.as<float4>();
   v.hdriDist = nullptr;
   v.numLights = (int)lights.size();
   v.numEnvLights = (int)envLights.size();

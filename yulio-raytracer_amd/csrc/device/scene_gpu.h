@@ -53,7 +53,7 @@ struct DevBuf {
 struct GpuScene {
   int device = 0;
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels,
-      lights, envLights, hdriDist;
+      lights, envLights, hdriDist, media;
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x for every material type used (shade kernel variant)
   // host mirrors (BVH export, precomputed light sampling, stats)

@@ -168,9 +168,46 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
       const yrt_v3 L = cin.getV3();
       check(dev, yrtSetFloat3(dev, l, "L", L.x, L.y, L.z), "rtSetFloat3");
       addLight(l);
-    } else if (tag == "-pointlight" || tag == "-masked_pointlight" || tag == "-directionallight" ||
-               tag == "-dirlight" || tag == "-distantlight" || tag == "-spotlight") {
-      throw std::runtime_error(tag + ": light type outside the MI355X device's scope (SURVEY.md §2 row 13)");
+    } else if (tag == "-pointlight" || tag == "-masked_pointlight") {
+      // renderer.cpp:1035-1059
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "pointlight"), "rtNewLight");
+      const yrt_v3 P = cin.getV3(), I = cin.getV3();
+      check(dev, yrtSetFloat3(dev, l, "P", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "I", I.x, I.y, I.z), "rtSetFloat3");
+      if (tag == "-pointlight") {
+        addLight(l);
+      } else {
+        const int illumMask = cin.getInt(), shadowMask = cin.getInt();
+        check(dev, yrtCommit(dev, l), "rtCommit(light)");
+        YRTHandle prim = checkH(dev, yrtNewLightPrimitive(dev, l, nullptr, nullptr), "rtNewLightPrimitive");
+        check(dev, yrtSetInt1(dev, prim, "illumMask", illumMask), "rtSetInt1");
+        check(dev, yrtSetInt1(dev, prim, "shadowMask", shadowMask), "rtSetInt1");
+        check(dev, yrtCommit(dev, prim), "rtCommit(primitive)");
+        prims.push_back(prim);
+      }
+    } else if (tag == "-directionallight" || tag == "-dirlight") {
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "directionallight"), "rtNewLight");
+      const yrt_v3 D = cin.getV3(), E = cin.getV3();
+      check(dev, yrtSetFloat3(dev, l, "D", D.x, D.y, D.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "E", E.x, E.y, E.z), "rtSetFloat3");
+      addLight(l);
+    } else if (tag == "-distantlight") {
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "distantlight"), "rtNewLight");
+      const yrt_v3 D = cin.getV3(), Lc = cin.getV3();
+      check(dev, yrtSetFloat3(dev, l, "D", D.x, D.y, D.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "L", Lc.x, Lc.y, Lc.z), "rtSetFloat3");
+      check(dev, yrtSetFloat1(dev, l, "halfAngle", cin.getFloat()), "rtSetFloat1");
+      addLight(l);
+    } else if (tag == "-spotlight") {
+      YRTHandle l = checkH(dev, yrtNewLight(dev, "spotlight"), "rtNewLight");
+      const yrt_v3 P = cin.getV3(), D = cin.getV3(), I = cin.getV3();
+      const float angleMin = cin.getFloat(), angleMax = cin.getFloat();
+      check(dev, yrtSetFloat3(dev, l, "P", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "D", D.x, D.y, D.z), "rtSetFloat3");
+      check(dev, yrtSetFloat3(dev, l, "I", I.x, I.y, I.z), "rtSetFloat3");
+      check(dev, yrtSetFloat1(dev, l, "angleMin", angleMin), "rtSetFloat1");
+      check(dev, yrtSetFloat1(dev, l, "angleMax", angleMax), "rtSetFloat1");
+      addLight(l);
     } else if (tag == "-trianglelight") {
       const yrt_v3 P = cin.getV3(), U = cin.getV3(), V = cin.getV3(), L = cin.getV3();
       YRTHandle l = checkH(dev, yrtNewLight(dev, "trianglelight"), "rtNewLight");

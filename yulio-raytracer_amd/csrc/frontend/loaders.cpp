@@ -215,6 +215,10 @@ struct XMLLoader {
   static void need(const XMLp& x, size_t n, const char* what) {
     if (x->body.size() != n) throw std::runtime_error(x->loc + ": wrong " + what + " body");
   }
+  float f1(const XMLp& x) {
+    need(x, 1, "float");
+    return F(x, 0);
+  }
   yrt_v3 v3(const XMLp& x) {
     need(x, 3, "float3");
     return {F(x, 0), F(x, 1), F(x, 2)};
@@ -364,7 +368,36 @@ struct XMLLoader {
       prims.push_back(prim_light(l));
     } else if (x->name == "PointLight" || x->name == "SpotLight" || x->name == "DirectionalLight" ||
                x->name == "DistantLight") {
-      throw std::runtime_error(x->loc + ": " + x->name + " is outside the MI355X device's scope (SURVEY.md §2 row 13)");
+      // loadPointLight / loadSpotLight / loadDirectionalLight / loadDistantLight (xml_loader.cpp:274-324)
+      const yrt_affine sp = affine(x->child("AffineSpace"));
+      YRTHandle l;
+      if (x->name == "PointLight") {
+        const yrt_v3 I = v3(x->child("I"));
+        l = checkH(dev, yrtNewLight(dev, "pointlight"), "rtNewLight");
+        check(dev, yrtSetFloat3(dev, l, "P", sp.v[9], sp.v[10], sp.v[11]), "rtSetFloat3");
+        check(dev, yrtSetFloat3(dev, l, "I", I.x, I.y, I.z), "rtSetFloat3");
+      } else if (x->name == "SpotLight") {
+        const yrt_v3 I = v3(x->child("I"));
+        l = checkH(dev, yrtNewLight(dev, "spotlight"), "rtNewLight");
+        check(dev, yrtSetFloat3(dev, l, "P", sp.v[9], sp.v[10], sp.v[11]), "rtSetFloat3");
+        check(dev, yrtSetFloat3(dev, l, "D", sp.v[6], sp.v[7], sp.v[8]), "rtSetFloat3");
+        check(dev, yrtSetFloat3(dev, l, "I", I.x, I.y, I.z), "rtSetFloat3");
+        check(dev, yrtSetFloat1(dev, l, "angleMin", f1(x->child("angleMin"))), "rtSetFloat1");
+        check(dev, yrtSetFloat1(dev, l, "angleMax", f1(x->child("angleMax"))), "rtSetFloat1");
+      } else if (x->name == "DirectionalLight") {
+        const yrt_v3 E = v3(x->child("E"));
+        l = checkH(dev, yrtNewLight(dev, "directionallight"), "rtNewLight");
+        check(dev, yrtSetFloat3(dev, l, "D", sp.v[6], sp.v[7], sp.v[8]), "rtSetFloat3");
+        check(dev, yrtSetFloat3(dev, l, "E", E.x, E.y, E.z), "rtSetFloat3");
+      } else {
+        const yrt_v3 Lc = v3(x->child("L"));
+        l = checkH(dev, yrtNewLight(dev, "distantlight"), "rtNewLight");
+        check(dev, yrtSetFloat3(dev, l, "D", sp.v[6], sp.v[7], sp.v[8]), "rtSetFloat3");
+        check(dev, yrtSetFloat3(dev, l, "L", Lc.x, Lc.y, Lc.z), "rtSetFloat3");
+        check(dev, yrtSetFloat1(dev, l, "halfAngle", f1(x->child("halfAngle"))), "rtSetFloat1");
+      }
+      check(dev, yrtCommit(dev, l), "rtCommit(light)");
+      prims.push_back(prim_light(l));
     } else if (x->name == "TriangleMesh") {
       // loadTriangleMesh (xml_loader.cpp:432-459)
       YRTHandle mat = material(x->child("material"));

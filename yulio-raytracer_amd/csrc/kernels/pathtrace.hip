@@ -612,10 +612,47 @@ __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V
 
 // Material::shade for the in-scope materials (materials/*.h). May modify dg.Ns (Obj bump).
 template <unsigned MM>
-__device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, DG& dg, BRDFSet& bs) {
+__device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, int matId, int medium, DG& dg,
+                                               BRDFSet& bs) {
   bs.n = 0;
   if (!(MM & mat_bit(m.type))) return;
+  const float idBits = __int_as_float(matId);
   switch (m.type) {
+    case MAT_PLASTIC:
+      // p: pigment[0..2], eta[3], roughness[4], rcpRoughness[5], layer etait[6], etati[7], eta_[8]
+      add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[6], m.p[7]);
+      if (m.p[4] == 0.0f) add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[8], 1.0f);
+      else add_comp(bs, C_MICROFACET, BT_GLOSSY_REFLECTION, v3s(1.f), 1.0f, m.p[3], m.p[5]);
+      break;
+    case MAT_DIELECTRIC:
+      // outside -> inside when the ray travels in the outside medium (dielectric.h:42-52)
+      if (medium == m.media[0]) {
+        add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[8], 1.0f);
+        add_comp(bs, C_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3s(0.f), m.p[8]);
+      } else {
+        add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[9], 1.0f);
+        add_comp(bs, C_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3s(0.f), m.p[9]);
+      }
+      break;
+    case MAT_MIRROR:
+      add_comp(bs, C_REFLECTION, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
+      break;
+    case MAT_METAL:
+      // p: R[0..2], eta[3..5], k[6..8], roughness[9], rcpRoughness[10]
+      if (m.p[9] == 0.0f) add_comp(bs, C_CONDUCTOR, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), 0.f, 0.f, idBits);
+      else add_comp(bs, C_MICRO_COND, BT_GLOSSY_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[10], 0.f, idBits);
+      break;
+    case MAT_BRUSHED_METAL:
+      // p: R[0..2], eta[3..5], k[6..8], roughnessX[9], roughnessY[10], rcp[11], rcp[12]
+      if (m.p[9] == 0.0f || m.p[10] == 0.0f)
+        add_comp(bs, C_CONDUCTOR, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), 0.f, 0.f, idBits);
+      else
+        add_comp(bs, C_MICRO_ANISO, BT_GLOSSY_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[11], m.p[12], idBits);
+      break;
+    case MAT_VELVET:
+      add_comp(bs, C_MINNAERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[3]);
+      add_comp(bs, C_VELVETY, BT_DIFFUSE_REFLECTION, v3(m.p[4], m.p[5], m.p[6]), m.p[7]);
+      break;
     case MAT_MATTE:
       add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
       break;
@@ -738,6 +775,8 @@ __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V
 
 __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
   if (lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
+  if (lt.type == LIGHT_DISTANT)  // DistantLight::Le (distantlight.h:38-41)
+    return dot(-wo, ld3(lt.e1)) >= lt.bsphere[1] ? v3(lt.L[0], lt.L[1], lt.L[2]) : v3s(0.f);
   return hdri_Le(sv, lt, wo);
 }
 
@@ -762,6 +801,39 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
     }
     wi = d * rcpf_(tMax);
     pdf = 2.0f * tMax * tMax * tMax * rcpf_(fabsf(dDotNg));
+    return v3(lt.L[0], lt.L[1], lt.L[2]);
+  }
+  if (lt.type == LIGHT_POINT) {  // pointlight.h:36-42
+    const V3 d = ld3(lt.v0) - dg.P;
+    const float distance = length(d);
+    wi = d / distance;
+    pdf = distance * distance;
+    return v3(lt.L[0], lt.L[1], lt.L[2]);
+  }
+  if (lt.type == LIGHT_SPOT) {  // spotlight.h:41-52
+    const V3 d = ld3(lt.v0) - dg.P;
+    const float distance = length(d);
+    wi = d * rcpf_(distance);
+    pdf = distance * distance;
+    const float cosAngle = dot(wi, ld3(lt.e1));
+    const float cosMin = lt.bsphere[0], cosMax = lt.bsphere[1];
+    if (cosMin != cosMax) return v3(lt.L[0], lt.L[1], lt.L[2]) * clampf((cosAngle - cosMax) * rcpf_(cosMin - cosMax));
+    if (cosAngle > cosMin) return v3(lt.L[0], lt.L[1], lt.L[2]);
+    return v3s(0.f);
+  }
+  if (lt.type == LIGHT_DIRECTIONAL) {  // directionallight.h:31-33 (Sample3f pdf defaults to 1)
+    wi = ld3(lt.e1);
+    pdf = 1.0f;
+    return v3(lt.L[0], lt.L[1], lt.L[2]);
+  }
+  if (lt.type == LIGHT_DISTANT) {  // distantlight.h:46-50, uniformSampleCone (shapesampler.h:149-165)
+    const float angle = lt.bsphere[0];
+    const float phi = kTwoPi * sx;
+    const float cosTheta = 1.0f - sy * (1.0f - cosf(angle));
+    const float sinTheta = cos2sin(cosTheta);
+    const V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
+    pdf = rcpf_(4.0f * kPi * sqrf(sinf(0.5f * angle)));
+    wi = mul(frame(ld3(lt.e1)), l);
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
   pdf = 0.f;
@@ -792,7 +864,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
     unsigned* shadowCount = pb.counters + qcounter_index(depthLevel, 1, oseg);
     int path = 0;
     V3 org = v3s(0.f), dir = v3s(0.f), thr = v3s(0.f), L = v3s(0.f);
-    int meta = 0, depth = 0, rec = 0, pixelId = 0, s = 0;
+    int meta = 0, depth = 0, rec = 0, pixelId = 0, s = 0, medium = 0;
     bool ignoreVL = false, unbent = false, isHit = false, useDirect = false;
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
     DG dg;
@@ -819,6 +891,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       depth = meta & 255;
       ignoreVL = (meta >> 8) & 1;
       unbent = (meta >> 9) & 1;
+      medium = (meta >> 10) & 0xFFFF;  // LightPath::lastMedium as a medium-table index
       s = path / bi.numPixels;
       const int i = path - s * bi.numPixels;
       int x = 0, y = 0;
@@ -835,7 +908,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       } else {
         const int g = sv.triGeom[gid];
         const int mat = sv.geoms[g].material;
-        const bool wantT = mat >= 0 && sv.materials[mat].type == MAT_OBJ && sv.materials[mat].tex[4] >= 0;
+        const bool wantT = mat >= 0 && ((sv.materials[mat].type == MAT_OBJ && sv.materials[mat].tex[4] >= 0) ||
+                                        (MM & mat_bit(MAT_BRUSHED_METAL) && sv.materials[mat].type == MAT_BRUSHED_METAL));
         post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
         bool backfacing = false;
         if (dot(dg.Ng, dir) > 0.f) {
@@ -843,7 +917,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
           dg.Ng = -dg.Ng;
           dg.Ns = -dg.Ns;
         }
-        if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg, bs);
+        if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg.material, medium, dg, bs);
         if (!ignoreVL && dg.light >= 0 && !backfacing) {
           const GpuLight& al = sv.lights[dg.light];
           L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
@@ -875,7 +949,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
             Ls = light_sample(lt, dg, sx, sy, wi, pdf);
           }
           if (!(Ls == v3s(0.f) || pdf == 0.f)) {
-            const V3 brdf = set_eval<comps_of(MM)>(bs, wo, dg, wi, BT_DIFFUSE);
+            const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
             if (!(brdf == v3s(0.f))) {
               const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
               const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
@@ -919,15 +993,24 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         const float ss = samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec);
         float pdf;
         uint32_t type;
-        const V3 c = set_sample<comps_of(MM)>(bs, wo, dg, sx, sy, ss, nwi, pdf, type);
+        V3 c = set_sample<comps_of(MM)>(bs, sv.materials, wo, dg, sx, sy, ss, nwi, pdf, type);
         if (!(c == v3s(0.f) || pdf <= 0.f)) {
+          if (MM & mat_bit(MAT_DIELECTRIC)) {
+            // simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207)
+            const float4 T = sv.media[medium];
+            if (!(T.x == 1.f && T.y == 1.f && T.z == 1.f)) c = c * v3(powf(T.x, h.x), powf(T.y, h.x), powf(T.z, h.x));
+            if ((type & BT_TRANSMISSION) && dg.material >= 0) {
+              const GpuMaterial& mt = sv.materials[dg.material];
+              if (mt.type == MAT_DIELECTRIC) medium = medium == mt.media[1] ? mt.media[0] : mt.media[1];
+            }
+          }
           nthr = thr * c * rcpf_(pdf);
           const bool nIgnore = (type & BT_DIFFUSE) != 0;
           const bool nUnbent = unbent && (nwi == dir);
           // loop head of the next iteration: depth+1 < maxDepth holds; minContribution test
           if (!(reduce_max(nthr) < rp.minContribution)) {
             cont = true;
-            nmeta = (depth + 1) | ((nIgnore ? 1 : 0) << 8) | ((nUnbent ? 1 : 0) << 9);
+            nmeta = (depth + 1) | ((nIgnore ? 1 : 0) << 8) | ((nUnbent ? 1 : 0) << 9) | (medium << 10);
           }
         }
       }

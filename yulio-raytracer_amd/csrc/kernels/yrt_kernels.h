@@ -26,6 +26,7 @@ struct SceneView {
   const GpuLight* lights;
   const int* envLights;
   const float* hdriDist;
+  const float4* media;  // medium table (transmission.rgb, eta); [0] = vacuum (materials/medium.h)
   int* traceSpill;   // deep traversal-stack entries: YRT_TRACE_SPILL_INTS ints
   int numLights, numEnvLights, numNodes, numTris;
 };

@@ -4,16 +4,18 @@
 // operations (left-to-right Color*float products etc.) so the GPU and the oracle agree:
 //   postIntersect   shapes/trianglemesh_full.cpp:192-260, trianglemesh_normals.cpp:125-147,
 //                   shapes/triangle.h:69-78
-//   materials       materials/{matte,matte_textured,metallicpaint,obj,Uber,thindielectric}.h
+//   materials       materials/{matte,matte_textured,metallicpaint,obj,Uber,thindielectric,plastic,
+//                   dielectric,mirror,metal,brushedmetal,velvet}.h
 //   BRDFs           brdfs/{lambertian,dielectric,dielectriclayer,microfacet,specular,
-//                   transmission,optics}.h, brdfs/microfacet/{power_cosine_distribution,fresnel}.h
+//                   transmission,optics,reflection,conductor,minnaert,velvety}.h,
+//                   brdfs/microfacet/{power_cosine_distribution,anisotropic_power_cosine_distribution,fresnel}.h
 //   composition     brdfs/compositedbrdf.h:58-166
 //   lights          lights/{ambientlight,trianglelight}.h, lights/hdrilight.cpp
 //   textures        textures/{Bilinear,nearestneighbor}.h, texel decode
 //                   common/math/color_scalar.h:47 (byte * one_over_255)
-// Omitted reference features (no BASELINE config reaches them): motion blur, participating
-// media (every in-scope material has a vacuum/vacuum interface), metallic-paint glitter,
-// the backplate image; DESIGN.md lists them.
+// Omitted reference features (no BASELINE config reaches them): motion blur, metallic-paint
+// glitter, the Beckmann distributions (no material instantiates them), the backplate image;
+// DESIGN.md lists them.
 #pragma once
 
 #include "../common/yrt_gpu_types.h"
@@ -40,6 +42,14 @@ enum CompKind : int {
   C_MICROFACET = 5,       // Microfacet<FresnelDielectric(etai,etat),PowerCosine(n,Ns)> R, a=etai, b=etat, c=n
   C_TRANSMISSION = 6,     // Transmission(T)
   C_SPECULAR = 7,         // Specular(R, exp)                            a=exp
+  C_REFLECTION = 8,       // Reflection(R)
+  C_CONDUCTOR = 9,        // Conductor(R, eta, k)                        c=material id (eta, k)
+  C_MICRO_COND = 10,      // Microfacet<FresnelConductor,PowerCosine>    R, a=n, c=material id
+  C_MICRO_ANISO = 11,     // Microfacet<FresnelConductor,AnisotropicPowerCosine(Tx,nx,Ty,ny,Ns)>
+                          //                                             R, a=nx, b=ny, c=material id
+  C_MINNAERT = 12,        // Minnaert(R, b)                              a=b
+  C_VELVETY = 13,         // Velvety(R, f)                               a=f
+  C_DIEL_TRANS = 14,      // DielectricTransmission(etai, etat)          a=eta_
 };
 
 // Material-set specialization: the shade kernel is instantiated for a bitmask of material
@@ -52,9 +62,15 @@ __host__ __device__ constexpr unsigned comps_of(unsigned mats) {
          ((mats & mat_bit(3)) ? (comp_bit(1) | comp_bit(4)) : 0u) |                                 // MetallicPaint
          ((mats & mat_bit(4)) ? (comp_bit(6) | comp_bit(0) | comp_bit(7)) : 0u) |                   // Obj
          ((mats & mat_bit(5)) ? (comp_bit(0) | comp_bit(2) | comp_bit(1) | comp_bit(5)) : 0u) |     // Uber
-         ((mats & mat_bit(6)) ? (comp_bit(1) | comp_bit(3)) : 0u);                                  // ThinDielectric
+         ((mats & mat_bit(6)) ? (comp_bit(1) | comp_bit(3)) : 0u) |                                 // ThinDielectric
+         ((mats & mat_bit(7)) ? (comp_bit(4) | comp_bit(1) | comp_bit(5)) : 0u) |                   // Plastic
+         ((mats & mat_bit(8)) ? (comp_bit(1) | comp_bit(14)) : 0u) |                                // Dielectric
+         ((mats & mat_bit(9)) ? comp_bit(8) : 0u) |                                                 // Mirror
+         ((mats & mat_bit(10)) ? (comp_bit(9) | comp_bit(10)) : 0u) |                               // Metal
+         ((mats & mat_bit(11)) ? (comp_bit(9) | comp_bit(11)) : 0u) |                               // BrushedMetal
+         ((mats & mat_bit(12)) ? (comp_bit(12) | comp_bit(13)) : 0u);                               // Velvet
 }
-#define YRT_ALL_MATS 0x7Eu
+#define YRT_ALL_MATS 0x1FFEu
 
 struct Comp {
   int kind;
@@ -175,8 +191,39 @@ __device__ __forceinline__ V3 lambert_eval(V3 R, const DG& dg, V3 wi) {
   return R * kOneOverPi * clampf(dot(wi, dg.Ns));
 }
 
-// Microfacet<FresnelDielectric, PowerCosineDistribution>::eval (brdfs/microfacet.h:28-41)
-__device__ __forceinline__ V3 microfacet_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+// fresnelConductor (brdfs/optics.h:123-131), per channel in the reference's operation order
+__device__ __forceinline__ V3 fresnel_conductor(float cosi, V3 eta, V3 k) {
+  const V3 tmp = eta * eta + k * k;
+  const V3 e2c = 2.0f * eta * cosi;
+  const V3 Rpar = (tmp * cosi * cosi - e2c + v3s(1.0f)) * rcpv(tmp * cosi * cosi + e2c + v3s(1.0f));
+  const V3 Rper = (tmp - e2c + v3s(cosi * cosi)) * rcpv(tmp + e2c + v3s(cosi * cosi));
+  return 0.5f * (Rpar + Rper);
+}
+__device__ __forceinline__ V3 mat_eta(const GpuMaterial* __restrict__ mats, float id) {
+  const GpuMaterial& m = mats[__float_as_int(id)];
+  return v3(m.p[3], m.p[4], m.p[5]);
+}
+__device__ __forceinline__ V3 mat_k(const GpuMaterial* __restrict__ mats, float id) {
+  const GpuMaterial& m = mats[__float_as_int(id)];
+  return v3(m.p[6], m.p[7], m.p[8]);
+}
+
+// AnisotropicPowerCosineDistribution::eval (brdfs/microfacet/anisotropic_power_cosine_distribution.h:40-48)
+__device__ __forceinline__ float aniso_D(float nx, float ny, const DG& dg, V3 wh) {
+  const float norm2 = sqrtf((nx + 2) * (ny + 2)) * kOneOverTwoPi;
+  const float cosPhiH = dot(wh, dg.Tx);
+  const float sinPhiH = dot(wh, dg.Ty);
+  const float cosThetaH = dot(wh, dg.Ns);
+  const float R = sqrf(cosPhiH) + sqrf(sinPhiH);
+  if (R == 0.0f) return norm2;
+  const float n = (nx * sqrf(cosPhiH) + ny * sqrf(sinPhiH)) * rcpf_(R);
+  return norm2 * powf(fabsf(cosThetaH), n);
+}
+
+// Microfacet<Fresnel, Distribution>::eval (brdfs/microfacet.h:28-41) for the dielectric /
+// conductor Fresnel terms and the power-cosine / anisotropic power-cosine distributions
+__device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
+                                             V3 wi) {
   if (dot(wi, dg.Ng) <= 0) return v3s(0.0f);
   const float cosThetaO = dot(wo, dg.Ns);
   const float cosThetaI = dot(wi, dg.Ns);
@@ -184,13 +231,34 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, V3 wo, const DG& dg
   const V3 wh = normalize(wi + wo);
   const float cosThetaH = dot(wh, dg.Ns);
   const float cosTheta = dot(wi, wh);
-  const float F = fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr);
-  const float n = c.c;
-  const float norm2 = (n + 2) * kOneOverTwoPi;
-  const float D = norm2 * powf(fabsf(dot(wh, dg.Ns)), n);
+  V3 F;
+  if (c.kind == C_MICROFACET) F = v3s(fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr));
+  else F = fresnel_conductor(cosTheta, mat_eta(mats, c.c), mat_k(mats, c.c));
+  float D;
+  if (c.kind == C_MICRO_ANISO) {
+    D = aniso_D(c.a, c.b, dg, wh);
+  } else {
+    const float n = c.kind == C_MICROFACET ? c.c : c.a;
+    const float norm2 = (n + 2) * kOneOverTwoPi;
+    D = norm2 * powf(fabsf(dot(wh, dg.Ns)), n);
+  }
   const float G = fminf(fminf(1.0f, 2.0f * cosThetaH * cosThetaO * rcpf_(cosTheta)),
                         2.0f * cosThetaH * cosThetaI * rcpf_(cosTheta));
-  return c.R * D * G * v3s(F) * rcpf_(4.0f * cosThetaO);
+  return c.R * D * G * F * rcpf_(4.0f * cosThetaO);
+}
+
+// Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26)
+__device__ __forceinline__ V3 minnaert_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  const float cosThetaI = clampf(dot(wi, dg.Ns));
+  const float backScatter = powf(clampf(dot(wo, wi)), c.a);
+  return c.R * backScatter * cosThetaI / kPi;
+}
+__device__ __forceinline__ V3 velvety_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  const float cosThetaO = clampf(dot(wo, dg.Ns));
+  const float cosThetaI = clampf(dot(wi, dg.Ns));
+  const float sinThetaO = sqrtf(1.0f - cosThetaO * cosThetaO);
+  const float horizonScatter = powf(sinThetaO, c.a);
+  return c.R * horizonScatter * cosThetaI / kPi;
 }
 
 // DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38), T = one
@@ -215,21 +283,27 @@ __device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, 
 }
 
 template <unsigned CM>
-__device__ __forceinline__ V3 comp_eval(const Comp c, V3 wo, const DG& dg, V3 wi) {
+__device__ __forceinline__ V3 comp_eval(const Comp c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
+                                        V3 wi) {
   if (!(CM & comp_bit(c.kind))) return v3s(0.0f);
   switch (c.kind) {
     case C_LAMBERT: return lambert_eval(c.R, dg, wi);
     case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
-    case C_MICROFACET: return microfacet_eval(c, wo, dg, wi);
+    case C_MICROFACET:
+    case C_MICRO_COND:
+    case C_MICRO_ANISO: return microfacet_eval(c, mats, wo, dg, wi);
     case C_SPECULAR: return specular_eval(c, wo, dg, wi);
+    case C_REFLECTION: return c.R;  // Reflection::eval (reflection.h:16-18)
+    case C_MINNAERT: return minnaert_eval(c, wo, dg, wi);
+    case C_VELVETY: return velvety_eval(c, wo, dg, wi);
     default: return v3s(0.0f);
   }
 }
 
 // BRDF::sample of one component; returns color, sets wi/pdf.
 template <unsigned CM>
-__device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, float sx, float sy, V3& wi,
-                                          float& pdf) {
+__device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
+                                          float sx, float sy, V3& wi, float& pdf) {
   if (!(CM & comp_bit(c.kind))) {
     pdf = 0.0f;
     wi = v3s(0.0f);
@@ -299,7 +373,72 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, flo
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
-      return microfacet_eval(c, wo, dg, wi);
+      return microfacet_eval(c, mats, wo, dg, wi);
+    }
+    case C_MICRO_COND: {
+      // Microfacet::sample (microfacet.h:43-50) with PowerCosineDistribution::sample
+      pdf = 0.0f;
+      if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
+      const float n = c.a;
+      const float norm1 = (n + 1) * kOneOverTwoPi;
+      const float phi = kTwoPi * sx;
+      const float cosPhi = cosf(phi);
+      const float sinPhi = sinf(phi);
+      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float sinTheta = cos2sin(cosTheta);
+      V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+      float whpdf = norm1 * powf(cosTheta, n);
+      wi = reflect2(wo, wh);
+      pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
+      if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
+      return microfacet_eval(c, mats, wo, dg, wi);
+    }
+    case C_MICRO_ANISO: {
+      // AnisotropicPowerCosineDistribution::sample (:57-73)
+      pdf = 0.0f;
+      if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
+      const float nx = c.a, ny = c.b;
+      const float norm1 = sqrtf((nx + 1) * (ny + 1)) * kOneOverTwoPi;
+      const float phi = kTwoPi * sx;
+      const float sinPhi0 = sqrtf(nx + 1) * sinf(phi);
+      const float cosPhi0 = sqrtf(ny + 1) * cosf(phi);
+      const float nrm = rsqrtf_(sqrf(sinPhi0) + sqrf(cosPhi0));
+      const float sinPhi = sinPhi0 * nrm;
+      const float cosPhi = cosPhi0 * nrm;
+      const float n = nx * sqrf(cosPhi) + ny * sqrf(sinPhi);
+      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float sinTheta = cos2sin(cosTheta);
+      const float whpdf = norm1 * powf(cosTheta, n);
+      const V3 h = v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta);
+      const V3 wh = h.x * dg.Tx + h.y * dg.Ty + h.z * dg.Ns;
+      wi = reflect2(wo, wh);
+      pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
+      if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
+      return microfacet_eval(c, mats, wo, dg, wi);
+    }
+    case C_REFLECTION: {  // reflection.h:19-22
+      wi = reflect2(wo, dg.Ns);
+      pdf = 1.0f;
+      return c.R;
+    }
+    case C_CONDUCTOR: {  // conductor.h:21-24
+      wi = reflect2(wo, dg.Ns);
+      pdf = 1.0f;
+      return c.R * fresnel_conductor(dot(wo, dg.Ns), mat_eta(mats, c.c), mat_k(mats, c.c));
+    }
+    case C_MINNAERT: {
+      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      return minnaert_eval(c, wo, dg, wi);
+    }
+    case C_VELVETY: {
+      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      return velvety_eval(c, wo, dg, wi);
+    }
+    case C_DIEL_TRANS: {  // dielectric.h:82-89 (the sample's eta is dropped)
+      const float cosThetaO = clampf(dot(wo, dg.Ns));
+      float cosThetaI;
+      pdf = refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaI, wi);
+      return v3s(1.0f - fresnel3(cosThetaO, cosThetaI, c.a));
     }
     case C_TRANSMISSION: {
       wi = -wo;
@@ -324,13 +463,14 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, V3 wo, const DG& dg, flo
 
 // CompositedBRDF::eval restricted to `type` (compositedbrdf.h:59-65)
 template <unsigned CM>
-__device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V3 wi, uint32_t type) {
+__device__ __forceinline__ V3 set_eval(const BRDFSet& bs, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
+                                       V3 wi, uint32_t type) {
   V3 c = v3s(0.0f);
 #pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i)
     if (i < bs.n && (bs.c[i].type & type)) {
       const Comp ci = bs.c[i];
-      c = c + comp_eval<CM>(ci, wo, dg, wi);
+      c = c + comp_eval<CM>(ci, mats, wo, dg, wi);
     }
   return c;
 }
@@ -340,8 +480,8 @@ __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, V3 wo, const DG& dg, V
 // running sum, CDF with the last entry forced to 1), written with compile-time component
 // indices only so nothing is spilled to scratch.
 template <unsigned CM>
-__device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg, float sx, float sy, float ss,
-                                         V3& wi_o, float& pdf_o, uint32_t& type_o) {
+__device__ __forceinline__ V3 set_sample(const BRDFSet& bs, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
+                                         float sx, float sy, float ss, V3& wi_o, float& pdf_o, uint32_t& type_o) {
   float f[YRT_MAX_COMPS];
   V3 colors[YRT_MAX_COMPS];
   V3 dirs[YRT_MAX_COMPS];
@@ -359,7 +499,7 @@ __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, V3 wo, const DG& dg,
       V3 wi;
       float pdf = 0.0f;
       const Comp ci = bs.c[i];
-      const V3 c = comp_sample<CM>(ci, wo, dg, sx, sy, wi, pdf);
+      const V3 c = comp_sample<CM>(ci, mats, wo, dg, sx, sy, wi, pdf);
       if (!((c.x == 0.0f && c.y == 0.0f && c.z == 0.0f) || pdf <= 0.0f)) {
         ok[i] = true;
         f[i] = (c.x + c.y + c.z) * rcpf_(pdf);
