@@ -1204,10 +1204,10 @@ void oracle_pixel_sets(int width, int height, int sets, uint8_t* out) {
 
 /* ====================================================================== camera */
 typedef struct {
-  int stereo, face, toeIn;
+  int stereo, face, toeIn, dof;
   A3 p2w[6];
   V3 origin, up, xyz;
-  float eyeSep, rcpZpd, falloff;
+  float eyeSep, rcpZpd, falloff, lensRadius, focal;
 } Camera;
 
 static int camera_build(const Blob* B, Camera* C) {
@@ -1219,6 +1219,17 @@ static int camera_build(const Blob* B, Camera* C) {
     const float angle = p_float(o, "angle", 64.0f), ar = p_float(o, "aspectRatio", 1.0f);
     const V3 W = xfmVector(l2w, v3(-0.5f * ar, -0.5f, 0.5f * rcp(tanf(deg2rad(0.5f * angle)))));
     C->p2w[0] = a3(l3(muls(l2w.l.vx, ar), l2w.l.vy, W), l2w.p);
+    return 0;
+  }
+  if (!strcasecmp(o->type, "depthoffield")) { /* cameras/depthoffieldcamera.h:13-19 */
+    const float angle = p_float(o, "angle", 64.0f), ar = p_float(o, "aspectRatio", 1.0f);
+    const V3 W = xfmVector(l2w, v3(-0.5f * ar, -0.5f, 0.5f * rcp(tanf(deg2rad(0.5f * angle)))));
+    C->p2w[0] = a3(l3(muls(l2w.l.vx, ar), l2w.l.vy, W), l2w.p);
+    C->p2w[1] = l2w;
+    C->dof = 1;
+    C->lensRadius = p_float(o, "lensRadius", 0.0f);
+    C->focal = p_float(o, "focalDistance", 0.0f) /
+               length(add(add(muls(C->p2w[0].l.vx, 0.5f), muls(C->p2w[0].l.vy, 0.5f)), C->p2w[0].l.vz));
     return 0;
   }
   if (strcasecmp(o->type, "stereo")) return fail("camera type outside the oracle's scope");
@@ -1252,7 +1263,16 @@ static int camera_build(const Blob* B, Camera* C) {
   return 0;
 }
 
-static void camera_ray(const Camera* C, float fx, float fy, V3* org, V3* dir) {
+static void camera_ray(const Camera* C, float fx, float fy, float lx, float ly, V3* org, V3* dir) {
+  if (C->dof) { /* depthoffieldcamera.h:20-26, uniformSampleDisk (shapesampler.h:187-191) */
+    const A3 m = C->p2w[0];
+    const float r = sqrtf(lx), th = TWO_PI_F * ly;
+    const V3 begin = xfmPoint(C->p2w[1], v3(C->lensRadius * r * cosf(th), C->lensRadius * r * sinf(th), 0.0f));
+    const V3 end = add(m.p, muls(add(add(muls(m.l.vx, fx), muls(m.l.vy, 1.0f - fy)), m.l.vz), C->focal));
+    *org = begin;
+    *dir = normalize(sub(end, begin));
+    return;
+  }
   if (!C->stereo) { /* pinholecamera.h:23-25 */
     const A3 m = C->p2w[0];
     *org = m.p;
@@ -2013,7 +2033,8 @@ static void* worker(void* arg) {
           const float fx = ((float)x + J->T->t[rec]) * rcpW;
           const float fy = ((float)y + J->T->t[(size_t)J->T->rec + rec]) * rcpH;
           Ray ray;
-          camera_ray(J->C, fx, fy, &ray.org, &ray.dir);
+          camera_ray(J->C, fx, fy, J->T->t[(size_t)2 * J->T->rec + rec], J->T->t[(size_t)3 * J->T->rec + rec], &ray.org,
+                     &ray.dir); /* sample.getLens() */
           ray.tnear = 0.f;
           ray.tfar = INFINITY;
           L = add(L, Li(J->W, J->R, J->T, rec, ray, (uint32_t)(y * J->width + x), s, J->seed, &nc, &ns));
@@ -2054,7 +2075,7 @@ static void debug_render(const World* W, const RCfg* R, const Camera* C, int wid
         if (ix >= width) continue;
         for (int i = 0; i < R->spp; i++) {
           Ray ray;
-          camera_ray(C, fx, fy, &ray.org, &ray.dir);
+          camera_ray(C, fx, fy, 0.f, 0.f, &ray.org, &ray.dir);
           ray.tnear = 0.f;
           ray.tfar = INFINITY;
           int id0 = -1, id1 = -1;

@@ -62,3 +62,26 @@ def test_materials_lights_parity(gpu_device, depth):
     ref, _ = oracle.render(s.export_frame(), 96, 72, s.info()["gamma"])
     parity(img, ref, 0.995, mad_rel=2e-4)
     s.close()
+
+
+def test_depth_of_field_camera_object(host_device):
+    """-radius r selects DepthOfFieldCamera (renderer.cpp:312-331): lensRadius r and the
+    focal distance |lookAt - position|."""
+    s = yrt.Session(ARGS + ["-size", "24", "18", "-radius", "6"], device=host_device)
+    objs = dae_scene.blob_objects(s.export_frame())
+    cam = [o for o in objs if o[0] == "CAMERA"][0]
+    assert cam[1] == "depthoffield" and cam[2]["lensRadius"][0] == 6.0
+    assert cam[2]["focalDistance"][0] == pytest.approx(float(np.linalg.norm([0, 440, 720])), rel=1e-6)
+    assert np.isfinite(oracle.render(s.export_frame(), 24, 18, 1.0)[0]).all()
+    s.close()
+
+
+@pytest.mark.gpu
+def test_depth_of_field_parity(gpu_device):
+    """Thin-lens rays from the sampler's lens dimensions (sample.getLens()), GPU vs oracle."""
+    s = yrt.Session(ARGS + ["-size", "80", "60", "-spp", "8", "-radius", "12", "-fb", "RGB_FLOAT32"],
+                    device=gpu_device)
+    img = s.render()
+    ref, _ = oracle.render(s.export_frame(), 80, 60, s.info()["gamma"])
+    parity(img, ref, 0.995, mad_rel=2e-4)
+    s.close()

@@ -116,7 +116,9 @@ struct GpuRenderParams {
 };
 
 // Camera (cameras/pinholecamera.h:15-21, cameras/StereoCubeCamera.h:16-65).
-enum CameraType : int32_t { CAM_PINHOLE = 0, CAM_STEREO = 1 };
+// CAM_DOF (cameras/depthoffieldcamera.h): p2w[0] pixel2world, p2w[1] local2world,
+// xyzStraight[0] lensRadius, xyzStraight[1] focalDistance (normalized)
+enum CameraType : int32_t { CAM_PINHOLE = 0, CAM_STEREO = 1, CAM_DOF = 2 };
 struct GpuCamera {
   int32_t type, cubeFaceIndex, toeIn, pad;
   float p2w[6][12];           // pixel2world[face]: vx, vy, vz, p (column-major)

@@ -469,8 +469,8 @@ static bool ieq(const char* a, const char* b) { return a && b && strcasecmp(a, b
 
 YRTHandle yrtNewCamera(YRTDevice dev, const char* type) {
   DEV_GUARD(dev, nullptr)
-  if (!ieq(type, "pinhole") && !ieq(type, "stereo"))
-    throw std::runtime_error(std::string("camera type '") + type + "' is outside the MI355X device's scope");
+  if (!ieq(type, "pinhole") && !ieq(type, "depthoffield") && !ieq(type, "stereo"))
+    throw std::runtime_error(std::string("unknown camera type: ") + type);
   return dev->d->wrap(std::make_shared<CameraObj>(type));
   DEV_END(nullptr)
 }

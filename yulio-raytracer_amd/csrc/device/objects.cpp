@@ -447,6 +447,18 @@ void CameraObj::commit() {
     const float aspectRatio = parms.getFloat("aspectRatio", 1.0f);
     const V3 W = xfmVector(l2w, v3(-0.5f * aspectRatio, -0.5f, 0.5f * rcpf_(tanf(deg2rad(0.5f * angle)))));
     store(cam.p2w[0], a3(l3(aspectRatio * l2w.l.vx, l2w.l.vy, W), l2w.p));
+  } else if (ieq(type, "depthoffield")) {
+    // cameras/depthoffieldcamera.h:13-19 over the pinhole setup
+    cam.type = CAM_DOF;
+    const A3 l2w = parms.getTransform("local2world");
+    const float angle = parms.getFloat("angle", 64.0f);
+    const float aspectRatio = parms.getFloat("aspectRatio", 1.0f);
+    const V3 W = xfmVector(l2w, v3(-0.5f * aspectRatio, -0.5f, 0.5f * rcpf_(tanf(deg2rad(0.5f * angle)))));
+    const A3 p2w = a3(l3(aspectRatio * l2w.l.vx, l2w.l.vy, W), l2w.p);
+    store(cam.p2w[0], p2w);
+    store(cam.p2w[1], l2w);
+    cam.xyzStraight[0] = parms.getFloat("lensRadius", 0.0f);
+    cam.xyzStraight[1] = parms.getFloat("focalDistance", 0.0f) / length(0.5f * p2w.l.vx + 0.5f * p2w.l.vy + p2w.l.vz);
   } else if (ieq(type, "stereo")) {
     // cameras/StereoCubeCamera.h:16-51
     cam.type = CAM_STEREO;

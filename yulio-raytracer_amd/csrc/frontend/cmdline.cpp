@@ -242,10 +242,8 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
     else if (tag == "-vd") { yrt_v3 d = cin.getV3(); camLookAt = {camPos.x + d.x, camPos.y + d.y, camPos.z + d.z}; }
     else if (tag == "-vu") camUp = cin.getV3();
     else if (tag == "-angle" || tag == "-fov") camFieldOfView = cin.getFloat();
-    else if (tag == "-radius") {
-      camRadius = cin.getFloat();
-      if (camRadius != 0.0f) throw std::runtime_error("-radius (depth-of-field camera) is outside the MI355X device's scope");
-    } else if (tag == "-stereo") stereo = true;
+    else if (tag == "-radius") camRadius = cin.getFloat();
+    else if (tag == "-stereo") stereo = true;
     else if (tag == "-toeIn") toeIn = true;
     else if (tag == "-waterMark") waterMark = true;
     else if (tag == "-eyeSeparation") eyeSeparation = cin.getFloat();
@@ -343,10 +341,16 @@ YRTHandle RtState::createCamera(int face) {
   const yrt_affine space = look_at(camPos, camLookAt, camUp);
   YRTHandle c;
   if (face < 0) {
-    c = checkH(dev, yrtNewCamera(dev, "pinhole"), "rtNewCamera");
+    // pinhole, or the depth-of-field camera when -radius != 0 (renderer.cpp:312-331)
+    c = checkH(dev, yrtNewCamera(dev, camRadius == 0.0f ? "pinhole" : "depthoffield"), "rtNewCamera");
     check(dev, yrtSetTransform(dev, c, "local2world", space.v), "rtSetTransform");
     check(dev, yrtSetFloat1(dev, c, "angle", camFieldOfView), "rtSetFloat1");
     check(dev, yrtSetFloat1(dev, c, "aspectRatio", float(width) / float(height)), "rtSetFloat1");
+    if (camRadius != 0.0f) {
+      const float dx = camLookAt.x - camPos.x, dy = camLookAt.y - camPos.y, dz = camLookAt.z - camPos.z;
+      check(dev, yrtSetFloat1(dev, c, "lensRadius", camRadius), "rtSetFloat1");
+      check(dev, yrtSetFloat1(dev, c, "focalDistance", sqrtf(dx * dx + dy * dy + dz * dz)), "rtSetFloat1");
+    }
   } else {
     c = checkH(dev, yrtNewCamera(dev, "stereo"), "rtNewCamera");
     check(dev, yrtSetTransform(dev, c, "local2world", space.v), "rtSetTransform");

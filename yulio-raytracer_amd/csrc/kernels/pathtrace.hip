@@ -145,11 +145,24 @@ __device__ __forceinline__ A3 ldA3(const float* m) {
 // ---------------------------------------------------------------- cameras
 // PinHoleCamera::ray (cameras/pinholecamera.h:23-25)
 // StereoCubeCamera::ray (cameras/StereoCubeCamera.h:68-161)
-__device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3& dir) {
+// DepthOfFieldCamera::ray (cameras/depthoffieldcamera.h:20-26); (lx, ly) = the lens sample
+__device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3& dir, float lx = 0.f,
+                           float ly = 0.f) {
   if (cam.type == CAM_PINHOLE) {
     A3 p2w = ldA3(cam.p2w[0]);
     org = p2w.p;
     dir = normalize(fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
+    return;
+  }
+  if (cam.type == CAM_DOF) {
+    const A3 p2w = ldA3(cam.p2w[0]), l2w = ldA3(cam.p2w[1]);
+    const float lensRadius = cam.xyzStraight[0], focalDistance = cam.xyzStraight[1];
+    // uniformSampleDisk (samplers/shapesampler.h:187-191)
+    const float r = sqrtf(lx), theta = kTwoPi * ly;
+    const V3 begin = xfmPoint(l2w, v3(lensRadius * r * cosf(theta), lensRadius * r * sinf(theta), 0.0f));
+    const V3 end = p2w.p + focalDistance * (fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
+    org = begin;
+    dir = normalize(end - begin);
     return;
   }
   const A3 pixel2world = ldA3(cam.p2w[0]);
@@ -243,7 +256,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
         const int rec = set * rp.spp + s;
         const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
         const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
-        camera_ray(cam, fx, fy, org, dir);
+        camera_ray(cam, fx, fy, org, dir, samp(fv, 2, rec), samp(fv, 3, rec));  // sample.getLens()
       }
       // loop head of Li: depth < maxDepth and max(throughput)=1 >= minContribution
       valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
