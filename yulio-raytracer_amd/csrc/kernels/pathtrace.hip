@@ -390,6 +390,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             ro = org[q];
             rd = dir[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
+            ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
             best.t = rd.w;
             best.u = best.v = 0.f;
             best.tri = -1;
@@ -440,13 +441,43 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       if (has && curCnt == 0) {
         float t[4];
         int c[4];
-        box4(nodes + curIdx, r, best.t, t, c);
-        sort4(t, c);
+#ifndef YRT_ORDERED_PLANES
+// 2 (default): ordered planes for shadow rays only — k_trace<true> -2.5%, while in
+// k_trace<false> the six per-lane plane addresses cost more than the min/max they save
+// (+11%, 80 VGPRs); 1 = both, 0 = neither
+#define YRT_ORDERED_PLANES 2
+#endif
+        if (YRT_ORDERED_PLANES == 1 || (YRT_ORDERED_PLANES == 2 && ANY))
+          box4_ordered(nodes + curIdx, r, __float_as_int(ri.w), best.t, t, c);
+        else
+          box4(nodes + curIdx, r, best.t, t, c);
+#ifndef YRT_CHILD_ORDER
+// Child order: 3 (default) = closest-hit rays sort the hit children by entry distance, shadow
+// (any-hit) rays take them in the builder's slot order — front-to-back order buys an any-hit
+// ray nothing, and skipping the 5-comparator network cut k_trace<true> by 9% (profiles/r01).
+// 0 = sort both, 1 = nearest-first only / none for any-hit, 2 = nearest-first for both.
+#define YRT_CHILD_ORDER 3
+#endif
+        if (YRT_CHILD_ORDER == 0 || (YRT_CHILD_ORDER == 3 && !ANY)) sort4(t, c);
+        else if (YRT_CHILD_ORDER == 2 || (YRT_CHILD_ORDER == 1 && !ANY)) nearest4(t, c);
         // nearest hit child next; the other hits pushed farthest-first
         const float INF = __int_as_float(0x7f800000);
-        if (t[3] < INF) YRT_PUSH(c[3]);
-        if (t[2] < INF) YRT_PUSH(c[2]);
-        if (t[1] < INF) YRT_PUSH(c[1]);
+#ifndef YRT_FAST_PUSH
+#define YRT_FAST_PUSH 1  // shadow rays -4..9%, closest neutral (profiles/r01)
+#endif
+        if (YRT_FAST_PUSH && sp + 3 <= YRT_LDS_STACK) {
+          // all three candidates fit in free ring slots: store unconditionally, advance sp
+          // only past the hit ones (a store of a missed child lands on a free slot)
+          const int h3 = t[3] < INF, h2 = t[2] < INF, h1 = t[1] < INF;
+          stack[YRT_SLOT(sp)] = c[3];
+          stack[YRT_SLOT(sp + h3)] = c[2];
+          stack[YRT_SLOT(sp + h3 + h2)] = c[1];
+          sp += h3 + h2 + h1;
+        } else {
+          if (t[3] < INF) YRT_PUSH(c[3]);
+          if (t[2] < INF) YRT_PUSH(c[2]);
+          if (t[1] < INF) YRT_PUSH(c[1]);
+        }
         if (t[0] < INF) {
           curIdx = c[0] >> 5;
           curCnt = c[0] & 31;
