@@ -56,9 +56,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # YRT_DIST_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU (ranks share
+    # device local % device_count); the driver's multi-GPU runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("YRT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import yrt
     from yrt import standin
@@ -102,7 +110,7 @@ def main():
     fb_t = None
     if world > 1:
         stride = (3 * a.size + 3) // 4 * 4
-        fb_t = torch.empty(stride * a.size, dtype=torch.uint8, device="cuda")
+        fb_t = torch.empty(stride * a.size, dtype=torch.uint8, device="cuda" if backend == "nccl" else "cpu")
 
     def step():
         # weak scaling: the job is `world` progressive iterations of the C3 frame (sampler
@@ -146,8 +154,9 @@ def main():
     elapsed = time.perf_counter() - t0
     samples_total = float(a.size) * a.size * 2 ** int(np.ceil(np.log2(a.spp))) * a.steps * world
 
-    tot = torch.tensor([acc["rays"], acc["closest"], acc["shadow"]], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    tot = torch.tensor([acc["rays"], acc["closest"], acc["shadow"]], dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
