@@ -296,6 +296,8 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
     pb.segCap = qseg_capacity(pb.capacity);
     pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
+    // one light: shadow contributions are added by k_trace<true> itself (no resolve pass)
+    pb.fuseShadow = rp.numLights == 1 && !getenv("YRT_NO_SHADOW_FUSE");
 
     struct EvPair { hipEvent_t a, b; int kind; };
     std::vector<EvPair> evs;
@@ -324,12 +326,13 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         if (rp.numLights > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
+          const ShadowFuse sf{pb.sContrib, pb.qL[cur ^ 1], pb.pathL};
           launch_trace_any(sv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, stream);
+                           pb.sOcc, stream, pb.fuseShadow ? &sf : nullptr);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
             capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap);
-          launch_shadow_resolve(pb, d, rp.numLights, stream);
+          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, stream);
         }
       }
       launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,

@@ -304,13 +304,30 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_TRACE_WAVES
 #define YRT_TRACE_WAVES 6
 #endif
+// A finished shadow query: the occlusion flag, or (fused, PathBuffers::fuseShadow) the
+// light's contribution added to its path's radiance when unoccluded (k_shadow_resolve order).
+__device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restrict__ occOut, int q, bool occluded) {
+  if (sf.contrib) {
+    if (!occluded) {
+      const float4 c = sf.contrib[q];
+      const int tg = __float_as_int(c.w);
+      float4* Lp = tg >= 0 ? sf.qL + tg : sf.pathL + (-tg - 1);
+      const float4 l = *Lp;
+      *Lp = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
+    }
+  } else {
+    occOut[q] = occluded ? 1 : 0;
+  }
+}
+
 template <bool ANY>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
-                                                         int* __restrict__ occOut, int* __restrict__ spillBuf) {
+                                                         int* __restrict__ occOut, int* __restrict__ spillBuf,
+                                                         ShadowFuse sf) {
   __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
@@ -373,7 +390,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   while (true) {
     // retire lanes whose traversal is complete
     if (has && curCnt < 0 && pendCnt == 0) {
-      if (ANY) occOut[q] = 0;
+      if (ANY) shadow_done(sf, occOut, q, false);
       else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
       has = false;
     }
@@ -401,7 +418,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             // NaN tfar (tMaxShadowRay = inf): no hit, nothing to traverse
             has = rd.w >= ro.w;
             if (!has) {
-              if (ANY) occOut[q] = 0;
+              if (ANY) shadow_done(sf, occOut, q, false);
               else hitOut[q] = make_float4(best.t, 0.f, 0.f, __int_as_float(-1));
             }
           }
@@ -556,7 +573,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       }
 #endif
       if (ANY && found) {
-        occOut[q] = 1;
+        shadow_done(sf, occOut, q, true);
         has = false;
       }
     }
@@ -972,54 +989,6 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       }
     }
 
-    // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167)
-    for (int li = 0; li < numLights; ++li) {
-      bool pred = false;
-      V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
-      float tnear = 0.f, tfar = 0.f;
-      if (active && isHit && useDirect) {
-        const GpuLight& lt = sv.lights[li];
-        if ((lt.illumMask & dg.illumMask) != 0) {
-          V3 Ls;
-          float pdf;
-          if (lt.precomputed >= 0) {
-            const float* ls = fv.lightSamples + ((size_t)rec * fv.numLightSlots + lt.precomputed) * 8;
-            wi = v3(ls[0], ls[1], ls[2]);
-            pdf = ls[3];
-            Ls = v3(ls[4], ls[5], ls[6]);
-          } else {
-            const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
-            const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
-            Ls = light_sample(lt, dg, sx, sy, wi, pdf);
-          }
-          if (!(Ls == v3s(0.f) || pdf == 0.f)) {
-            const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
-            if (!(brdf == v3s(0.f))) {
-              const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
-              const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
-                                                  rp.tMaxShadowRay * rp.tMaxShadowJitter;
-              float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
-              const float dotProduct = dot(wi, ld3(rp.up));
-              if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
-              sOrg = dg.P;
-              tnear = dg.error * rp.epsilon;
-              tfar = tMax - dg.error * rp.epsilon;
-              contrib = thr * Ls * brdf * rcpf_(pdf);
-              pred = true;
-            }
-          }
-        }
-      }
-      bool got;
-      const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, got);
-      if (got) {
-        pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
-        pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
-        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, 0.f);
-      }
-      if (active) pb.shFirst[(size_t)q * numLights + li] = got ? (int)si : -1;
-    }
-
     // continuation (pathtraceintegrator.cpp:169-213)
     bool cont = false;
     V3 nwi = v3s(0.f), nthr = v3s(0.f);
@@ -1061,6 +1030,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
     }
     bool got;
     const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
+    // radiance target of this vertex's shadow rays (fused resolve, see ShadowFuse)
+    const int lTarget = got ? (int)nq : -(path + 1);
     if (got) {
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
@@ -1071,6 +1042,56 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);  // path ends here
     }
     if (active) pb.qNext[q] = got ? (int)nq : -1;
+
+    // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); emitted after
+    // the continuation so a fused shadow ray knows where its path's radiance lives
+    for (int li = 0; li < numLights; ++li) {
+      bool pred = false;
+      V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
+      float tnear = 0.f, tfar = 0.f;
+      if (active && isHit && useDirect) {
+        const GpuLight& lt = sv.lights[li];
+        if ((lt.illumMask & dg.illumMask) != 0) {
+          V3 Ls;
+          float pdf;
+          if (lt.precomputed >= 0) {
+            const float* ls = fv.lightSamples + ((size_t)rec * fv.numLightSlots + lt.precomputed) * 8;
+            wi = v3(ls[0], ls[1], ls[2]);
+            pdf = ls[3];
+            Ls = v3(ls[4], ls[5], ls[6]);
+          } else {
+            const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
+            const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
+            Ls = light_sample(lt, dg, sx, sy, wi, pdf);
+          }
+          if (!(Ls == v3s(0.f) || pdf == 0.f)) {
+            const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
+            if (!(brdf == v3s(0.f))) {
+              const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
+              const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
+                                                  rp.tMaxShadowRay * rp.tMaxShadowJitter;
+              float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
+              const float dotProduct = dot(wi, ld3(rp.up));
+              if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
+              sOrg = dg.P;
+              tnear = dg.error * rp.epsilon;
+              tfar = tMax - dg.error * rp.epsilon;
+              contrib = thr * Ls * brdf * rcpf_(pdf);
+              pred = true;
+            }
+          }
+        }
+      }
+      bool sgot;
+      const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
+      if (sgot) {
+        pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
+        pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
+        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(pb.fuseShadow ? lTarget : 0));
+      }
+      if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numLights + li] = sgot ? (int)si : -1;
+    }
+
   }
 }
 
@@ -1244,14 +1265,15 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
                           int numSegs, int segCap, float4* hit, hipStream_t s) {
   const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr, sv.traceSpill);
+                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{});
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s) {
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse) {
   const long long maxCount = (long long)numSegs * segCap;
   hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill);
+                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill,
+                     fuse ? *fuse : ShadowFuse{});
 }
 
 // Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of

@@ -85,6 +85,19 @@ struct PathBuffers {
   int capacity;        // max paths
   int segCap;          // closest-queue slots per segment (qPath/qOrg/qDir/hit: YRT_QSEGS * segCap)
   int shSegCap;        // shadow slots per segment (sOrg/sDir/sContrib/sOcc: YRT_QSEGS * shSegCap)
+  // 1 (one light): k_shade stores each shadow ray's radiance target in sContrib.w and
+  // k_trace<true> adds the contribution itself when the ray is unoccluded — one writer per
+  // path, so the sum is deterministic and in the reference's order; k_shadow_resolve is not
+  // launched. 0: sOcc + shFirst + k_shadow_resolve (several lights, light order kept).
+  int fuseShadow;
+};
+
+// Radiance target of a fused shadow ray (sContrib.w bits): >= 0 slot in the next closest
+// queue's qL, < 0 path id -(t+1) in pathL (the path ended at this vertex).
+struct ShadowFuse {
+  const float4* contrib;  // null: not fused, k_trace<true> writes occlusion flags
+  float4* qL;             // qL of the next closest queue
+  float4* pathL;
 };
 
 struct BatchInfo {
@@ -102,7 +115,7 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
                           int numSegs, int segCap, float4* hit, hipStream_t s);
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s);
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr);
 // materialMask: bit MAT_x set for every material type the scene uses (selects a specialized
 // instantiation of the shade kernel)
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
