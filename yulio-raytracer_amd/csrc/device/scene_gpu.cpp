@@ -215,6 +215,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     return S;
   }
   for (const GpuMaterial& m : materials) S->materialMask |= 1u << m.type;
+  for (const GpuLight& l : lights) S->materialMask |= 1u << (16 + l.type);  // light_bit (kernels/yrt_shade.h)
   S->nodes.upload(bvh.nodes);
   S->tris.upload(bvh.tris);
   S->triGeom.upload(triGeom);

@@ -55,7 +55,7 @@ struct GpuScene {
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels,
       lights, envLights, hdriDist, media;
   SceneView view{};
-  unsigned materialMask = 0;  // bit MAT_x for every material type used (shade kernel variant)
+  unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)
   // host mirrors (BVH export, precomputed light sampling, stats)
   std::vector<GpuNode> hNodes;
   std::vector<GpuTri> hTris;

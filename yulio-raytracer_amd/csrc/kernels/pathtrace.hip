@@ -834,21 +834,30 @@ __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V
   return r;
 }
 
+// YRT_SHADE_LIGHT_SPEC: the shade instantiation handles only the light types in bits 16.. of
+// its mask (LM = bit LIGHT_x); 0 = every type.
+#ifndef YRT_SHADE_LIGHT_SPEC
+#define YRT_SHADE_LIGHT_SPEC 0  // measured neutral-to-worse on C3 (A/B), kept off
+#endif
+#define YRT_LM(MM) (YRT_SHADE_LIGHT_SPEC ? ((MM) >> 16) : 0x7Fu)
+template <unsigned LM>
 __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
-  if (lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
-  if (lt.type == LIGHT_DISTANT)  // DistantLight::Le (distantlight.h:38-41)
+  if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
+  if ((LM & (1u << LIGHT_DISTANT)) && lt.type == LIGHT_DISTANT)  // DistantLight::Le (distantlight.h:38-41)
     return dot(-wo, ld3(lt.e1)) >= lt.bsphere[1] ? v3(lt.L[0], lt.L[1], lt.L[2]) : v3s(0.f);
-  return hdri_Le(sv, lt, wo);
+  if ((LM & (1u << LIGHT_HDRI)) && lt.type == LIGHT_HDRI) return hdri_Le(sv, lt, wo);
+  return v3s(0.f);
 }
 
 // Light::sample for a non-precomputed light; returns L, sets wi/pdf.
+template <unsigned LM>
 __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
-  if (lt.type == LIGHT_AMBIENT) {
+  if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) {
     // lights/ambientlight.h:52-65 (the bsphere tMax is overwritten by the integrator)
     wi = cosine_hemi(sx, sy, dg.Ns, pdf);
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
-  if (lt.type == LIGHT_TRIANGLE) {
+  if ((LM & (1u << LIGHT_TRIANGLE)) && lt.type == LIGHT_TRIANGLE) {
     // lights/trianglelight.h:77-85
     const V3 A = ld3(lt.v0), B = ld3(lt.v1), C = ld3(lt.v2);
     const float su = sqrtf(sx);
@@ -864,14 +873,14 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
     pdf = 2.0f * tMax * tMax * tMax * rcpf_(fabsf(dDotNg));
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
-  if (lt.type == LIGHT_POINT) {  // pointlight.h:36-42
+  if ((LM & (1u << LIGHT_POINT)) && lt.type == LIGHT_POINT) {  // pointlight.h:36-42
     const V3 d = ld3(lt.v0) - dg.P;
     const float distance = length(d);
     wi = d / distance;
     pdf = distance * distance;
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
-  if (lt.type == LIGHT_SPOT) {  // spotlight.h:41-52
+  if ((LM & (1u << LIGHT_SPOT)) && lt.type == LIGHT_SPOT) {  // spotlight.h:41-52
     const V3 d = ld3(lt.v0) - dg.P;
     const float distance = length(d);
     wi = d * rcpf_(distance);
@@ -882,12 +891,12 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
     if (cosAngle > cosMin) return v3(lt.L[0], lt.L[1], lt.L[2]);
     return v3s(0.f);
   }
-  if (lt.type == LIGHT_DIRECTIONAL) {  // directionallight.h:31-33 (Sample3f pdf defaults to 1)
+  if ((LM & (1u << LIGHT_DIRECTIONAL)) && lt.type == LIGHT_DIRECTIONAL) {  // directionallight.h:31-33 (Sample3f pdf defaults to 1)
     wi = ld3(lt.e1);
     pdf = 1.0f;
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
-  if (lt.type == LIGHT_DISTANT) {  // distantlight.h:46-50, uniformSampleCone (shapesampler.h:149-165)
+  if ((LM & (1u << LIGHT_DISTANT)) && lt.type == LIGHT_DISTANT) {  // distantlight.h:46-50, uniformSampleCone (shapesampler.h:149-165)
     const float angle = lt.bsphere[0];
     const float phi = kTwoPi * sx;
     const float cosTheta = 1.0f - sy * (1.0f - cosf(angle));
@@ -965,7 +974,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       if (!isHit) {
         // environment shading (pathtraceintegrator.cpp:79-92); backplate not supported
         if (!ignoreVL)
-          for (int j = 0; j < sv.numEnvLights; ++j) L = L + thr * env_Le(sv, sv.lights[sv.envLights[j]], wo);
+          for (int j = 0; j < sv.numEnvLights; ++j) L = L + thr * env_Le<YRT_LM(MM)>(sv, sv.lights[sv.envLights[j]], wo);
       } else {
         const int g = sv.triGeom[gid];
         const int mat = sv.geoms[g].material;
@@ -1062,7 +1071,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
           } else {
             const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
             const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
-            Ls = light_sample(lt, dg, sx, sy, wi, pdf);
+            Ls = light_sample<YRT_LM(MM)>(lt, dg, sx, sy, wi, pdf);
           }
           if (!(Ls == v3s(0.f) || pdf == 0.f)) {
             const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
@@ -1277,13 +1286,16 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
 }
 
 // Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of
-// the scene's materials; YRT_ALL_MATS is the generic fallback.
-static const unsigned kShadeVariants[] = {
-    mat_bit(MAT_UBER),                                                                // Collada (Sponza)
-    mat_bit(MAT_OBJ),                                                                 // OBJ scenes
-    mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT),                                 // cornell spheres
-    mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT),    // test_stereo
-    YRT_ALL_MATS};
+// the scene's material and light types; YRT_SV_ALL is the generic fallback.
+// Bits 16.. select the light types (light_bit); the first four cover the reference's scenes
+// (dome / quad / HDRI lights).
+#define YRT_SV_UBER (mat_bit(MAT_UBER) | YRT_BASIC_LIGHTS)                                   // Collada (Sponza)
+#define YRT_SV_OBJ (mat_bit(MAT_OBJ) | YRT_BASIC_LIGHTS)                                     // OBJ scenes
+#define YRT_SV_SPHERES (mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT) | YRT_BASIC_LIGHTS)  // cornell spheres
+#define YRT_SV_STEREO \
+  (mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT) | YRT_BASIC_LIGHTS)  // test_stereo
+#define YRT_SV_ALL (YRT_ALL_MATS | YRT_ALL_LIGHTS)
+static const unsigned kShadeVariants[] = {YRT_SV_UBER, YRT_SV_OBJ, YRT_SV_SPHERES, YRT_SV_STEREO, YRT_SV_ALL};
 
 template <unsigned MM>
 static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
@@ -1294,23 +1306,18 @@ static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathB
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
                   unsigned materialMask, hipStream_t s) {
-  unsigned pick = YRT_ALL_MATS;
+  unsigned pick = YRT_SV_ALL;
   for (unsigned v : kShadeVariants)
     if ((materialMask & ~v) == 0) {
       pick = v;
       break;
     }
   switch (pick) {
-    case mat_bit(MAT_UBER): launch_shade_t<mat_bit(MAT_UBER)>(sv, fv, pb, bi, depth, s); break;
-    case mat_bit(MAT_OBJ): launch_shade_t<mat_bit(MAT_OBJ)>(sv, fv, pb, bi, depth, s); break;
-    case mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT):
-      launch_shade_t<mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT)>(sv, fv, pb, bi, depth, s);
-      break;
-    case mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT):
-      launch_shade_t<mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT)>(sv, fv, pb, bi,
-                                                                                                   depth, s);
-      break;
-    default: launch_shade_t<YRT_ALL_MATS>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_UBER: launch_shade_t<YRT_SV_UBER>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s); break;
+    default: launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s); break;
   }
 }
 

@@ -71,6 +71,10 @@ __host__ __device__ constexpr unsigned comps_of(unsigned mats) {
          ((mats & mat_bit(12)) ? (comp_bit(12) | comp_bit(13)) : 0u);                               // Velvet
 }
 #define YRT_ALL_MATS 0x1FFEu
+// Light types ride in bits 16.. of the same instantiation mask (bit 16 + LIGHT_x).
+__host__ __device__ constexpr unsigned light_bit(int t) { return 1u << (16 + t); }
+#define YRT_BASIC_LIGHTS (light_bit(0) | light_bit(1) | light_bit(2))  // ambient, triangle, HDRI
+#define YRT_ALL_LIGHTS 0x7F0000u
 
 struct Comp {
   int kind;
@@ -221,7 +225,13 @@ __device__ __forceinline__ float aniso_D(float nx, float ny, const DG& dg, V3 wh
 }
 
 // Microfacet<Fresnel, Distribution>::eval (brdfs/microfacet.h:28-41) for the dielectric /
-// conductor Fresnel terms and the power-cosine / anisotropic power-cosine distributions
+// conductor Fresnel terms and the power-cosine / anisotropic power-cosine distributions.
+// YRT_MICRO_SPEC: CM (the kernel's component set) compiles out the conductor / anisotropic
+// branches no material of the scene can create.
+#ifndef YRT_MICRO_SPEC
+#define YRT_MICRO_SPEC 1  // k_shade -5% on C3 (same-box A/B, profiles/r01)
+#endif
+template <unsigned CM>
 __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
                                              V3 wi) {
   if (dot(wi, dg.Ng) <= 0) return v3s(0.0f);
@@ -231,14 +241,17 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* 
   const V3 wh = normalize(wi + wo);
   const float cosThetaH = dot(wh, dg.Ns);
   const float cosTheta = dot(wi, wh);
+  constexpr bool kCond = !YRT_MICRO_SPEC || (CM & (comp_bit(C_MICRO_COND) | comp_bit(C_MICRO_ANISO))) != 0;
+  constexpr bool kAniso = !YRT_MICRO_SPEC || (CM & comp_bit(C_MICRO_ANISO)) != 0;
+  const bool diel = !kCond || c.kind == C_MICROFACET;
   V3 F;
-  if (c.kind == C_MICROFACET) F = v3s(fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr));
+  if (diel) F = v3s(fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr));
   else F = fresnel_conductor(cosTheta, mat_eta(mats, c.c), mat_k(mats, c.c));
   float D;
-  if (c.kind == C_MICRO_ANISO) {
+  if (kAniso && c.kind == C_MICRO_ANISO) {
     D = aniso_D(c.a, c.b, dg, wh);
   } else {
-    const float n = c.kind == C_MICROFACET ? c.c : c.a;
+    const float n = diel ? c.c : c.a;
     const float norm2 = (n + 2) * kOneOverTwoPi;
     D = norm2 * powf(fabsf(dot(wh, dg.Ns)), n);
   }
@@ -291,7 +304,7 @@ __device__ __forceinline__ V3 comp_eval(const Comp c, const GpuMaterial* __restr
     case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
     case C_MICROFACET:
     case C_MICRO_COND:
-    case C_MICRO_ANISO: return microfacet_eval(c, mats, wo, dg, wi);
+    case C_MICRO_ANISO: return microfacet_eval<CM>(c, mats, wo, dg, wi);
     case C_SPECULAR: return specular_eval(c, wo, dg, wi);
     case C_REFLECTION: return c.R;  // Reflection::eval (reflection.h:16-18)
     case C_MINNAERT: return minnaert_eval(c, wo, dg, wi);
@@ -373,7 +386,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
-      return microfacet_eval(c, mats, wo, dg, wi);
+      return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_MICRO_COND: {
       // Microfacet::sample (microfacet.h:43-50) with PowerCosineDistribution::sample
@@ -391,7 +404,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
-      return microfacet_eval(c, mats, wo, dg, wi);
+      return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_MICRO_ANISO: {
       // AnisotropicPowerCosineDistribution::sample (:57-73)
@@ -414,7 +427,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
-      return microfacet_eval(c, mats, wo, dg, wi);
+      return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_REFLECTION: {  // reflection.h:19-22
       wi = reflect2(wo, dg.Ns);
