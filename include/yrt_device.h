@@ -148,14 +148,16 @@ typedef struct YRTRenderStats {
 YRT_API int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out);
 /* 1 = bracket every kernel with HIP events (adds sync-free event records). */
 YRT_API int yrtSetKernelTiming(YRTDevice dev, int enable);
-/* Scene info: triangles, geometries, BVH nodes, BVH depth, build seconds. */
+/* Scene info: triangles, geometries, BVH nodes, BVH depth, build seconds; numTriRefs = leaf
+ * triangle records (>= numTriangles: spatial splits reference a triangle from several leaves). */
 typedef struct YRTSceneInfo {
   int64_t numTriangles, numGeometries, numNodes, bvhDepth, numLights;
   double buildSeconds;
   float bboxLo[3], bboxHi[3];
+  int64_t numTriRefs;
 } YRTSceneInfo;
 YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
-/* Copies the host mirror of the BVH (4-wide nodes: 128 B each, tris: 48 B each) for tests. */
+/* Copies the host mirror of the BVH (4-wide nodes: 128 B each, numTriRefs leaf tris: 48 B each). */
 YRT_API int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes, void* tris,
                          size_t trisBytes);
 /* Serializes the committed scene graph + renderer + camera as the oracle's input blob

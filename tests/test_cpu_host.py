@@ -131,14 +131,20 @@ def _incoherent(blob, n, seed=42):
     return org4, dir4
 
 
+@pytest.mark.parametrize("sbvh", [0, 1], ids=["sah", "sbvh"])
 @pytest.mark.parametrize("which", ["C1", "C2", "C3", "C4"])
-def test_device_bvh_gives_oracle_hits(host_device, which):
-    """The product's SAH BVH (csrc/device/bvh_build.cpp), traversed in the device kernel's
+def test_device_bvh_gives_oracle_hits(host_device, which, sbvh, monkeypatch):
+    """The product's SAH BVH (csrc/device/bvh_build.cpp; sbvh: with spatial splits, triangles
+    referenced from several leaves with clipped boxes), traversed in the device kernel's
     order by the oracle, returns the same closest hits as the oracle's own BVH: the
     (t, triangle id) tie-break makes the hit independent of the tree."""
+    monkeypatch.setenv("YRT_SBVH", str(sbvh))
     args = {"C1": c1_args(32), "C2": c2_args(32, 1), "C3": c3_args(32, 1),
             "C4": c4_args(32, 1, stereo=False)}[which]
     s = yrt.Session(args, device=host_device)
+    if sbvh:
+        info = host_device.scene_info(s.info()["scene"])
+        assert info["numTriRefs"] >= info["numTriangles"]
     scene = s.info()["scene"]
     blob = s.export_frame()
     nodes, tris = host_device.export_bvh(scene)

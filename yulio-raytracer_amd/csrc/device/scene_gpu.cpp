@@ -261,8 +261,13 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     int gcount = 0;
     for (size_t i = 0; i < prims.size(); ++i)
       if (prims[i] && prims[i]->shape) S->slotGeom[i] = gcount++;
-    std::vector<int> leafOf(gidBase);
-    for (int i = 0; i < gidBase; ++i) leafOf[bvh.order[i]] = i;
+    // gid -> leaf slots (CSR: gidBase + 1 offsets, then the slots; spatial splits can put a
+    // triangle in several leaves)
+    std::vector<int> leafOf(gidBase + 1 + bvh.order.size(), 0);
+    for (int g : bvh.order) leafOf[g + 1]++;
+    for (int g = 0; g < gidBase; ++g) leafOf[g + 1] += leafOf[g];
+    std::vector<int> fill(leafOf.begin(), leafOf.begin() + gidBase);
+    for (size_t i = 0; i < bvh.order.size(); ++i) leafOf[gidBase + 1 + fill[bvh.order[i]]++] = (int)i;
     S->triLeaf.upload(leafOf);
     std::vector<std::vector<int>> levels;
     std::vector<std::pair<int, int>> work = {{0, 0}};
@@ -326,7 +331,7 @@ bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>&
     HIP_CHECK(hipMemcpyAsync(S.normals.as<float4>() + g.vtxBase, nor.data(), nor.size() * sizeof(float4),
                              hipMemcpyHostToDevice, stream));
     launch_refit_tris(S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(), S.triLeaf.as<int>(),
-                      g.triBase, (int)(m.tri.size() / 3), stream);
+                      S.triLeaf.as<int>() + S.numTris + 1, g.triBase, (int)(m.tri.size() / 3), stream);
     // the host copies must outlive the async copies
     HIP_CHECK(hipStreamSynchronize(stream));
   }

@@ -1390,17 +1390,21 @@ namespace yrt {
 // to a rebuild's: the closest hit is the smallest (t, triangle id) whatever the tree.
 __global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ tris, const int4* __restrict__ indices,
                                                          const float4* __restrict__ positions,
-                                                         const int* __restrict__ triLeaf, int firstTri, int numTris) {
+                                                         const int* __restrict__ leafStart,
+                                                         const int* __restrict__ leafSlots, int firstTri, int numTris) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= numTris) return;
   const int gid = firstTri + i;
   const int4 ix = indices[gid];
   const float4 a = positions[ix.x], b = positions[ix.y], c = positions[ix.z];
-  GpuTri& t = tris[triLeaf[gid]];
-  // e1 = v0 - v1, e2 = v2 - v0 (device/bvh_build.cpp, rtcore convention); .w words kept
-  t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z;
-  t.e1[0] = a.x - b.x; t.e1[1] = a.y - b.y; t.e1[2] = a.z - b.z;
-  t.e2[0] = c.x - a.x; t.e2[1] = c.y - a.y; t.e2[2] = c.z - a.z;
+  // every leaf slot referencing the triangle (spatial splits duplicate references)
+  for (int k = leafStart[gid]; k < leafStart[gid + 1]; ++k) {
+    GpuTri& t = tris[leafSlots[k]];
+    // e1 = v0 - v1, e2 = v2 - v0 (device/bvh_build.cpp, rtcore convention); .w words kept
+    t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z;
+    t.e1[0] = a.x - b.x; t.e1[1] = a.y - b.y; t.e1[2] = a.z - b.z;
+    t.e2[0] = c.x - a.x; t.e2[1] = c.y - a.y; t.e2[2] = c.z - a.z;
+  }
 }
 
 __global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes(GpuNode* __restrict__ nodes, const GpuTri* __restrict__ tris,
@@ -1441,11 +1445,11 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes(GpuNode* __restrict__
   }
 }
 
-void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* triLeaf, int firstTri,
-                       int numTris, hipStream_t s) {
+void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* leafStart,
+                       const int* leafSlots, int firstTri, int numTris, hipStream_t s) {
   if (numTris <= 0) return;
   hipLaunchKernelGGL(k_refit_tris, dim3((numTris + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, tris, indices,
-                     positions, triLeaf, firstTri, numTris);
+                     positions, leafStart, leafSlots, firstTri, numTris);
 }
 
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,

@@ -127,9 +127,10 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 int trace_profile(unsigned long long* out8, int reset);
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s);
 // BVH refit after faceCamera updates: rewrite triangles [firstTri, firstTri+numTris) (global
-// ids) from the vertex buffer, then refit one tree level of nodes (call deepest level first)
-void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* triLeaf, int firstTri,
-                       int numTris, hipStream_t s);
+// ids) from the vertex buffer in every leaf slot that references them (leafSlots[leafStart[g]
+// .. leafStart[g+1])), then refit one tree level of nodes (call deepest level first)
+void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* leafStart,
+                       const int* leafSlots, int firstTri, int numTris, hipStream_t s);
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
                         const int* levelNodes, int count, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,

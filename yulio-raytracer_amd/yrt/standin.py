@@ -10,6 +10,7 @@ any scene (devices/device/loaders/xml_loader.cpp restated in csrc/frontend/loade
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 import numpy as np
@@ -208,7 +209,7 @@ def write_xml(path: Path | None = None) -> Path:
         out.append("          <float2 name=\"s0\">0 0</float2>\n          <float2 name=\"ds\">1 1</float2>")
         out.append("        </parameters>\n      </material>\n    </TriangleMesh>")
     out += ["  </Group>", "</scene>", ""]
-    tmp = path.with_suffix(".tmp")
+    tmp = path.with_suffix(f".{os.getpid()}.tmp")  # per process: concurrent writers never share it
     tmp.write_text("\n".join(out))
     tmp.replace(path)
     return path
