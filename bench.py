@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=48, help="rows of the centred CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
+    p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
     return p.parse_args()
 
 
@@ -81,6 +82,8 @@ def main():
     R, S, T, F = info["renderer"], info["scene"], info["tonemapper"], info["framebuffer"]
     sinfo = dev.scene_info(S)
     dev.set_tile_shard(rank, world)
+    if a.capacity:
+        dev.set_batch_capacity(a.capacity)
 
     # ---- untimed capture frame: visit counts of the real query streams (roofline bytes)
     import oracle

@@ -166,7 +166,7 @@ YRT_API int64_t yrtExportFrame(YRTDevice dev, YRTHandle renderer, YRTHandle came
                                size_t bytes);
 /* Frame seed of the shadow-jitter hash (replaces C rand(), pathtraceintegrator.cpp:151). */
 YRT_API int yrtSetFrameSeed(YRTDevice dev, uint32_t seed);
-/* Paths in flight per wavefront batch (default 16M); smaller for tests. */
+/* Paths in flight per wavefront batch (default 64M, ~10 GB of wavefront state); smaller for tests. */
 YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
 /* Tile sharding for multi-GPU: render only tiles with (tileIndex % count) == index. */
 YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);

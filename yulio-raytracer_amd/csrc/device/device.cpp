@@ -42,7 +42,7 @@ class Device {
   int hipDevice = 0;
   hipStream_t stream = nullptr;
   uint32_t frameSeed = 0x2545F491u;
-  int64_t capacity = 16ll << 20;
+  int64_t capacity = 64ll << 20;  // paths per batch: C3 +4 % over 16 M (fewer launch tails), ~10 GB
   int shardIndex = 0, shardCount = 1;
   bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
   bool kernelTiming = false;
