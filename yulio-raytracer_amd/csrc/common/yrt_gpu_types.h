@@ -79,9 +79,14 @@ struct GpuImage {
   int32_t width, height, format, pad;
   int64_t offset;   // byte offset into the texel pool
 };
+// The image's descriptor is repeated in the texture record so a texel fetch is one dependent
+// load after the material (material -> texture -> texels) instead of two.
 struct GpuTexture {
-  int32_t image, filter, invert, pad;
+  int32_t image, filter, invert, width;
+  int32_t height, format;
+  int64_t offset;  // byte offset of the image in the texel pool
 };
+static_assert(sizeof(GpuTexture) == 32, "texture record is 32 B");
 
 enum LightType : int32_t {
   LIGHT_AMBIENT = 0,

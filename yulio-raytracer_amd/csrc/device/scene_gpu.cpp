@@ -61,6 +61,10 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     GpuTexture g;
     memset(&g, 0, sizeof(g));
     g.image = imageId(t->image);
+    g.width = images[g.image].width;
+    g.height = images[g.image].height;
+    g.format = images[g.image].format;
+    g.offset = images[g.image].offset;
     g.filter = t->filter;
     g.invert = t->invert ? 1 : 0;
     textures.push_back(g);

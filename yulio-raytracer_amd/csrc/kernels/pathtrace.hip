@@ -584,7 +584,11 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 // BackendSceneFlat::postIntersect -> Shape::postIntersect
 __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
                                bool wantTangents) {
+#if YRT_SHADE_FLAT
+  const int g = sv.indices[gid].w;  // geometry id rides in the index record
+#else
   const int g = sv.triGeom[gid];
+#endif
   const GpuGeom geom = sv.geoms[g];
   dg.material = geom.material;
   dg.light = geom.light;
@@ -976,7 +980,11 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         if (!ignoreVL)
           for (int j = 0; j < sv.numEnvLights; ++j) L = L + thr * env_Le<YRT_LM(MM)>(sv, sv.lights[sv.envLights[j]], wo);
       } else {
+#if YRT_SHADE_FLAT
+        const int g = sv.indices[gid].w;
+#else
         const int g = sv.triGeom[gid];
+#endif
         const int mat = sv.geoms[g].material;
         const bool wantT = mat >= 0 && ((sv.materials[mat].type == MAT_OBJ && sv.materials[mat].tex[4] >= 0) ||
                                         (MM & mat_bit(MAT_BRUSHED_METAL) && sv.materials[mat].type == MAT_BRUSHED_METAL));

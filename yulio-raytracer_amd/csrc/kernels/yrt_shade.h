@@ -151,12 +151,25 @@ __device__ __forceinline__ void texel(const GpuImage& im, const uint8_t* __restr
   c[3] = im.format == IMG_RGB8 ? 1.0f : b.w * one_over_255;
 }
 
+// YRT_SHADE_FLAT: the texture record's own image descriptor and the triangle's geometry id
+// from its index record (indices[gid].w) — one dependent load fewer on each shading chain.
+#ifndef YRT_SHADE_FLAT
+#define YRT_SHADE_FLAT 1
+#endif
 // Texture::get (textures/Bilinear.h:8-25, textures/nearestneighbor.h:25-32) -> RGBA
 __device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures, const GpuImage* __restrict__ images,
                                         const uint8_t* __restrict__ pool, int texId, float px, float py,
                                         float out[4]) {
   const GpuTexture tx = textures[texId];
+#if YRT_SHADE_FLAT
+  GpuImage im;
+  im.width = tx.width;
+  im.height = tx.height;
+  im.format = tx.format;
+  im.offset = tx.offset;
+#else
   const GpuImage im = images[tx.image];
+#endif
   const float s1 = px - floorf(px), t1 = py - floorf(py);
   float c[4];
   if (tx.filter == TEX_BILINEAR) {
