@@ -81,7 +81,7 @@ class Device {
 
   // per-frame device state
   DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCounters, dCount;
-  DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], qL[2], qNext, hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc;
+  DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc;
   int64_t pathCap = 0, shadowCap = 0;
   FrameCache fcache;
   std::vector<hipEvent_t> eventPool;
@@ -127,9 +127,7 @@ class Device {
         qOrg[k].alloc(Q * 16);
         qDir[k].alloc(Q * 16);
         qThr[k].alloc(Q * 16);
-        qL[k].alloc(Q * 16);
       }
-      qNext.alloc(Q * 4);
       hit.alloc(Q * 16);
       pathL.alloc(Q * 16);
       pathCap = Q;
@@ -282,9 +280,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     }
     for (int k = 0; k < 2; ++k) {
       pb.qThr[k] = qThr[k].as<float4>();
-      pb.qL[k] = qL[k].as<float4>();
     }
-    pb.qNext = qNext.as<int>();
     pb.hit = hit.as<float4>();
     pb.pathL = pathL.as<float4>();
     pb.shFirst = shFirst.as<int>();
@@ -326,7 +322,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         if (rp.numLights > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
-          const ShadowFuse sf{pb.sContrib, pb.qL[cur ^ 1], pb.pathL};
+          const ShadowFuse sf{pb.sContrib, pb.pathL};
           launch_trace_any(sv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
                            pb.sOcc, stream, pb.fuseShadow ? &sf : nullptr);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }

@@ -269,7 +269,6 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
       pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
       pb.qThr[0][q] = make_float4(1.f, 1.f, 1.f, __int_as_float((0) | (0 << 8) | (1 << 9)));
-      pb.qL[0][q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -311,7 +310,7 @@ __device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restric
     if (!occluded) {
       const float4 c = sf.contrib[q];
       const int tg = __float_as_int(c.w);
-      float4* Lp = tg >= 0 ? sf.qL + tg : sf.pathL + (-tg - 1);
+      float4* Lp = sf.pathL + tg;
       const float4 l = *Lp;
       *Lp = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
     }
@@ -940,6 +939,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
     V3 org = v3s(0.f), dir = v3s(0.f), thr = v3s(0.f), L = v3s(0.f);
     int meta = 0, depth = 0, rec = 0, pixelId = 0, s = 0, medium = 0;
     bool ignoreVL = false, unbent = false, isHit = false, useDirect = false;
+    bool haveL = false;  // L holds pathL[path] plus this vertex's emission (written back below)
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
     DG dg;
     BRDFSet bs;
@@ -958,9 +958,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       org = v3(o.x, o.y, o.z);
       dir = v3(d.x, d.y, d.z);
       h = pb.hit[q];
-      const float4 t4 = pb.qThr[cur][q], l4 = pb.qL[cur][q];
+      const float4 t4 = pb.qThr[cur][q];
       thr = v3(t4.x, t4.y, t4.z);
-      L = v3(l4.x, l4.y, l4.z);
       meta = __float_as_int(t4.w);
       depth = meta & 255;
       ignoreVL = (meta >> 8) & 1;
@@ -978,7 +977,10 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       if (!isHit) {
         // environment shading (pathtraceintegrator.cpp:79-92); backplate not supported
         if (!ignoreVL)
-          for (int j = 0; j < sv.numEnvLights; ++j) L = L + thr * env_Le<YRT_LM(MM)>(sv, sv.lights[sv.envLights[j]], wo);
+          for (int j = 0; j < sv.numEnvLights; ++j) {
+            if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
+            L = L + thr * env_Le<YRT_LM(MM)>(sv, sv.lights[sv.envLights[j]], wo);
+          }
       } else {
 #if YRT_SHADE_FLAT
         const int g = sv.indices[gid].w;
@@ -998,6 +1000,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg.material, medium, dg, bs);
         if (!ignoreVL && dg.light >= 0 && !backfacing) {
           const GpuLight& al = sv.lights[dg.light];
+          if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
           L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
         }
 #pragma unroll
@@ -1047,21 +1050,16 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
     }
     bool got;
     const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
-    // radiance target of this vertex's shadow rays (fused resolve, see ShadowFuse)
-    const int lTarget = got ? (int)nq : -(path + 1);
+    if (haveL) pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);
     if (got) {
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
       pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
       pb.qThr[cur ^ 1][nq] = make_float4(nthr.x, nthr.y, nthr.z, __int_as_float(nmeta));
-      pb.qL[cur ^ 1][nq] = make_float4(L.x, L.y, L.z, 0.f);
-    } else if (active) {
-      pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);  // path ends here
     }
-    if (active) pb.qNext[q] = got ? (int)nq : -1;
 
-    // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); emitted after
-    // the continuation so a fused shadow ray knows where its path's radiance lives
+    // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); its
+    // contribution is added to pathL[path] after the emission above (reference order)
     for (int li = 0; li < numLights; ++li) {
       bool pred = false;
       V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
@@ -1104,7 +1102,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       if (sgot) {
         pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
         pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
-        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(pb.fuseShadow ? lTarget : 0));
+        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
       }
       if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numLights + li] = sgot ? (int)si : -1;
     }
@@ -1123,9 +1121,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, in
     bool any = false;
     for (int li = 0; li < numLights; ++li) any |= pb.shFirst[(size_t)q * numLights + li] >= 0;
     if (!any) continue;
-    // the path's radiance now lives in the next queue (continued) or in pathL (ended)
-    const int nq = pb.qNext[q];
-    float4* Lp = nq >= 0 ? &pb.qL[cur ^ 1][nq] : &pb.pathL[pb.qPath[cur][q]];
+    float4* Lp = &pb.pathL[pb.qPath[cur][q]];
     const float4 l4 = *Lp;
     V3 L = v3(l4.x, l4.y, l4.z);
     for (int li = 0; li < numLights; ++li) {

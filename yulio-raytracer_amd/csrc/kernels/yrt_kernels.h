@@ -65,17 +65,16 @@ inline __host__ __device__ int qseg_capacity(long long items) {
 }
 
 // Wavefront state for one batch of P = numPixels * spp paths (SoA, device memory).
-// Path state travels with the queue entry (coalesced in queue order); only the final
-// radiance is scattered to the path-indexed pathL, once, when a path terminates.
+// Path state travels with the queue entry (coalesced in queue order); radiance lives in the
+// path-indexed pathL and is only touched when a vertex adds emission or direct light.
 struct PathBuffers {
   int* qPath[2];
   float4* qOrg[2];   // xyz, tnear
   float4* qDir[2];   // xyz, tfar
   float4* qThr[2];   // throughput xyz, w = meta bits: depth | ignoreVL<<8 | unbent<<9
-  float4* qL[2];     // radiance so far (xyz)
-  int* qNext;        // per closest-queue slot: slot of the continuation in the next queue, -1 = ended
   float4* hit;       // t, u, v, tri (bits), per closest-queue slot
-  float4* pathL;     // per path id: final radiance
+  float4* pathL;     // per path id: radiance so far (emission and unoccluded direct light are
+                     // read-modify-written in the reference's order; one writer per path at a time)
   int* shFirst;      // per (queue slot, light): shadow-ray slot or -1
   float4* sOrg;      // shadow rays
   float4* sDir;
@@ -85,18 +84,16 @@ struct PathBuffers {
   int capacity;        // max paths
   int segCap;          // closest-queue slots per segment (qPath/qOrg/qDir/hit: YRT_QSEGS * segCap)
   int shSegCap;        // shadow slots per segment (sOrg/sDir/sContrib/sOcc: YRT_QSEGS * shSegCap)
-  // 1 (one light): k_shade stores each shadow ray's radiance target in sContrib.w and
-  // k_trace<true> adds the contribution itself when the ray is unoccluded — one writer per
-  // path, so the sum is deterministic and in the reference's order; k_shadow_resolve is not
+  // 1 (one light): k_shade stores each shadow ray's path id in sContrib.w and k_trace<true>
+  // adds the contribution to pathL itself when the ray is unoccluded — one writer per path,
+  // so the sum is deterministic and in the reference's order; k_shadow_resolve is not
   // launched. 0: sOcc + shFirst + k_shadow_resolve (several lights, light order kept).
   int fuseShadow;
 };
 
-// Radiance target of a fused shadow ray (sContrib.w bits): >= 0 slot in the next closest
-// queue's qL, < 0 path id -(t+1) in pathL (the path ended at this vertex).
+// Fused shadow resolve: sContrib.w = path id (bits) whose pathL receives the contribution.
 struct ShadowFuse {
   const float4* contrib;  // null: not fused, k_trace<true> writes occlusion flags
-  float4* qL;             // qL of the next closest queue
   float4* pathL;
 };
 
