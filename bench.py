@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--size", type=int, default=2048)
     p.add_argument("--spp", type=int, default=64)
-    p.add_argument("--cpu-rows", type=int, default=48, help="rows of the centred CPU-baseline sample")
+    p.add_argument("--cpu-rows", type=int, default=112, help="rows of the centred CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
     p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
