@@ -187,6 +187,20 @@ def test_oracle_thumbnails_golden(host_device, name, args):
     s.close()
 
 
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_oracle_hit_records_golden(host_device, name):
+    """KAT 4: the oracle's closest hits (t, u, v, triangle id) and occlusion flags for 4096
+    incoherent rays stay bit-identical to the committed records (tests/golden/make_golden.py)."""
+    g = np.load(GOLDEN / f"hits_{name}_4096.npz")
+    args = {"c2": c2_args(32, 1), "c3": c3_args(32, 1)}[name]
+    s = yrt.Session(args, device=host_device)
+    blob = s.export_frame()
+    assert np.array_equal(oracle.trace(blob, g["org"], g["dir"]).view(np.uint32), g["hit"].view(np.uint32))
+    assert np.array_equal(oracle.trace(blob, g["org"], g["occ_dir"], any_hit=True)[:, 3].view(np.int32), g["occ"])
+    assert (g["hit"][:, 3].view(np.int32) >= 0).mean() > 0.5 and 0 < g["occ"].mean() < 1
+    s.close()
+
+
 def test_oracle_debug_renderer_golden(host_device):
     g = np.load(GOLDEN / "debug_c2_64.npy")
     s = yrt.Session(c2_args(64, 1) + ["-renderer", "debug", "-fb", "RGB_FLOAT32"], device=host_device)

@@ -86,6 +86,34 @@ def test_intersect_and_occluded(gpu_device, which):
     s.close()
 
 
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_intersect_golden_records(gpu_device, name):
+    """KAT 4 on the device: yrtIntersect / yrtOccluded on the committed incoherent rays give
+    the committed triangle ids and occlusion flags bit-exactly, t/u/v within 1e-5."""
+    import torch
+    from pathlib import Path
+    g = np.load(Path(__file__).parent / "golden" / f"hits_{name}_4096.npz")
+    args = {"c2": c2_args(32, 1), "c3": c3_args(32, 1)}[name]
+    s = _session(gpu_device, args)
+    scene = s.info()["scene"]
+    n = len(g["org"])
+    o = torch.from_numpy(g["org"]).cuda()
+    dd = torch.from_numpy(g["dir"]).cuda()
+    do = torch.from_numpy(g["occ_dir"]).cuda()
+    hit = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    occ = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    gpu_device.intersect(scene, o.data_ptr(), dd.data_ptr(), n, hit.data_ptr())
+    gpu_device.occluded(scene, o.data_ptr(), do.data_ptr(), n, occ.data_ptr())
+    h = hit.cpu().numpy()
+    ref = g["hit"]
+    assert np.array_equal(h[:, 3].view(np.int32), ref[:, 3].view(np.int32))
+    m = ref[:, 3].view(np.int32) >= 0
+    np.testing.assert_allclose(h[m, :3], ref[m, :3], rtol=1e-5, atol=1e-6)
+    assert np.array_equal(occ.cpu().numpy(), g["occ"])
+    s.close()
+
+
 # ----------------------------------------------------------------------------- full renders
 def test_c1_pathtracer_parity(gpu_device):
     img, ref, st = _render_pair(gpu_device, c1_args(256, 1))
