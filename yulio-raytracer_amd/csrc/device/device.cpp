@@ -53,7 +53,7 @@ class Device {
   std::vector<Captured> capClosest, capShadow;
   // counts: the queue's first segment counter; segments of segCap slots
   void capture(std::vector<Captured>& out, int depth, const float4* org, const float4* dir, const unsigned* counts,
-               int segCap) {
+               int segCap, hipStream_t stream) {
     std::vector<unsigned> cs((size_t)YRT_QSEGS * YRT_QCSTRIDE);
     HIP_CHECK(hipMemcpyAsync(cs.data(), counts, cs.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -80,9 +80,22 @@ class Device {
   }
 
   // per-frame device state
-  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCounters, dCount;
-  DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc;
-  int64_t pathCap = 0, shadowCap = 0;
+  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount;
+  // A wavefront lane: a stream and the batch state it owns. Batches alternate between the
+  // lanes so one batch's kernels run beside the other's (the VALU-bound traversal next to the
+  // latency-bound shading); lane 0's stream is also the device's stream for everything else.
+  struct Lane {
+    hipStream_t stream = nullptr;
+    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
+    int64_t pathCap = 0, shadowCap = 0;
+    unsigned* hc = nullptr;  // pinned copy of the counters of the lane's last batch
+    size_t hcWords = 0;
+    bool pending = false;    // a batch was enqueued whose counters are not yet accounted
+    int64_t pendTiles = 0;   // tiles done once that batch drains (progress)
+  };
+  static constexpr int kMaxLanes = 2;
+  Lane lanes[kMaxLanes];
+  int numLanes = kMaxLanes;
   FrameCache fcache;
   std::vector<hipEvent_t> eventPool;
 
@@ -90,12 +103,17 @@ class Device {
   explicit Device(int dev, bool useGpu) : hipDevice(dev), gpu(useGpu) {
     if (!gpu) return;
     HIP_CHECK(hipSetDevice(hipDevice));
-    HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (Lane& L : lanes) HIP_CHECK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    stream = lanes[0].stream;
+    if (const char* e = getenv("YRT_LANES")) numLanes = std::max(1, std::min(kMaxLanes, atoi(e)));
   }
   ~Device() {
     for (auto* h : handles) delete h;
     for (auto e : eventPool) (void)hipEventDestroy(e);
-    if (stream) (void)hipStreamDestroy(stream);
+    for (Lane& L : lanes) {
+      if (L.hc) (void)hipHostFree(L.hc);
+      if (L.stream) (void)hipStreamDestroy(L.stream);
+    }
   }
 
   YRTHandle wrap(std::shared_ptr<Object> o) {
@@ -119,27 +137,27 @@ class Device {
   }
 
   // P paths per batch; queues hold YRT_QSEGS segments of qseg_capacity(P) slots
-  void ensure_paths(int64_t P, int numLights) {
+  static void ensure_paths(Lane& L, int64_t P, int numLights) {
     const int64_t Q = (int64_t)YRT_QSEGS * qseg_capacity(P);
-    if (Q > pathCap) {
+    if (Q > L.pathCap) {
       for (int k = 0; k < 2; ++k) {
-        qPath[k].alloc(Q * 4);
-        qOrg[k].alloc(Q * 16);
-        qDir[k].alloc(Q * 16);
-        qThr[k].alloc(Q * 16);
+        L.qPath[k].alloc(Q * 4);
+        L.qOrg[k].alloc(Q * 16);
+        L.qDir[k].alloc(Q * 16);
+        L.qThr[k].alloc(Q * 16);
       }
-      hit.alloc(Q * 16);
-      pathL.alloc(Q * 16);
-      pathCap = Q;
+      L.hit.alloc(Q * 16);
+      L.pathL.alloc(Q * 16);
+      L.pathCap = Q;
     }
     const int64_t S = Q * std::max(1, numLights);
-    if (S > shadowCap) {
-      shFirst.alloc(S * 4);
-      sOrg.alloc(S * 16);
-      sDir.alloc(S * 16);
-      sContrib.alloc(S * 16);
-      sOcc.alloc(S * 4);
-      shadowCap = S;
+    if (S > L.shadowCap) {
+      L.shFirst.alloc(S * 4);
+      L.sOrg.alloc(S * 16);
+      L.sDir.alloc(S * 16);
+      L.sContrib.alloc(S * 16);
+      L.sOcc.alloc(S * 4);
+      L.shadowCap = S;
     }
   }
 
@@ -266,80 +284,63 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     const int spp = rp.spp;
     int64_t tilesPerBatch = std::max<int64_t>(1, capacity / (256ll * spp));
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
-    ensure_paths(std::max<int64_t>(P, 256ll * spp), rp.numLights);
+    const int64_t numBatches = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
+    // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
+    const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
     const size_t counterWords = qcounter_index(levels, 0, 0);
-    dCounters.alloc(counterWords * sizeof(unsigned));
     dAccu.alloc((size_t)W * H * 16);
-    std::vector<unsigned> hc(counterWords);
-    PathBuffers pb;
-    for (int k = 0; k < 2; ++k) {
-      pb.qPath[k] = qPath[k].as<int>();
-      pb.qOrg[k] = qOrg[k].as<float4>();
-      pb.qDir[k] = qDir[k].as<float4>();
-    }
-    for (int k = 0; k < 2; ++k) {
-      pb.qThr[k] = qThr[k].as<float4>();
-    }
-    pb.hit = hit.as<float4>();
-    pb.pathL = pathL.as<float4>();
-    pb.shFirst = shFirst.as<int>();
-    pb.sOrg = sOrg.as<float4>();
-    pb.sDir = sDir.as<float4>();
-    pb.sContrib = sContrib.as<float4>();
-    pb.sOcc = sOcc.as<int>();
-    pb.counters = dCounters.as<unsigned>();
-    pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
-    pb.segCap = qseg_capacity(pb.capacity);
-    pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
-    // one light: shadow contributions are added by k_trace<true> itself (no resolve pass)
-    pb.fuseShadow = rp.numLights == 1 && !getenv("YRT_NO_SHADOW_FUSE");
-
-    struct EvPair { hipEvent_t a, b; int kind; };
-    std::vector<EvPair> evs;
-    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch) {
-      if (R.stopFlag && R.stopFlag->load()) break;
-      BatchInfo bi;
-      bi.firstTile = (int)first;
-      bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
-      bi.tileStride = shardCount;
-      bi.tileOffset = shardIndex;
-      HIP_CHECK(hipMemsetAsync(dCounters.p, 0, counterWords * sizeof(unsigned), stream));
-      launch_raygen(fv, pb, bi, stream);
-      for (int d = 0; d < rp.maxDepth; ++d) {
-        const int cur = d & 1;
-        EvPair e1{};
-        if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, stream)); }
-        launch_trace_closest(sv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                             pb.segCap, pb.hit, stream);
-        if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, stream)); evs.push_back(e1); }
-        if (captureMax > 0 && first == 0)
-          capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap);
-        EvPair e2{};
-        if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, stream)); }
-        launch_shade(sv, fv, pb, bi, d, G.materialMask, stream);
-        if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, stream)); evs.push_back(e2); }
-        if (rp.numLights > 0) {
-          EvPair e3{};
-          if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, stream)); }
-          const ShadowFuse sf{pb.sContrib, pb.pathL};
-          launch_trace_any(sv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, stream, pb.fuseShadow ? &sf : nullptr);
-          if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, stream)); evs.push_back(e3); }
-          if (captureMax > 0 && first == 0)
-            capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap);
-          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, stream);
-        }
+    for (int l = 0; l < nl; ++l) {
+      Lane& L = lanes[l];
+      ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights);
+      L.counters.alloc(counterWords * sizeof(unsigned));
+      L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
+      if (L.hcWords < counterWords) {
+        if (L.hc) HIP_CHECK(hipHostFree(L.hc));
+        HIP_CHECK(hipHostMalloc((void**)&L.hc, counterWords * sizeof(unsigned), hipHostMallocDefault));
+        L.hcWords = counterWords;
       }
-      launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
-                            dAccu.as<float4>(), accumulate ? 1 : 0, stream);
-      HIP_CHECK(hipMemcpyAsync(hc.data(), dCounters.p, hc.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
-      HIP_CHECK(hipStreamSynchronize(stream));
+      L.pending = false;
+    }
+    // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
+    if (nl > 1) {
+      hipEvent_t setup = ev();
+      HIP_CHECK(hipEventRecord(setup, stream));
+      for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(lanes[l].stream, setup, 0));
+    }
+    auto lane_buffers = [&](Lane& L) {
+      PathBuffers pb;
+      for (int k = 0; k < 2; ++k) {
+        pb.qPath[k] = L.qPath[k].as<int>();
+        pb.qOrg[k] = L.qOrg[k].as<float4>();
+        pb.qDir[k] = L.qDir[k].as<float4>();
+        pb.qThr[k] = L.qThr[k].as<float4>();
+      }
+      pb.hit = L.hit.as<float4>();
+      pb.pathL = L.pathL.as<float4>();
+      pb.shFirst = L.shFirst.as<int>();
+      pb.sOrg = L.sOrg.as<float4>();
+      pb.sDir = L.sDir.as<float4>();
+      pb.sContrib = L.sContrib.as<float4>();
+      pb.sOcc = L.sOcc.as<int>();
+      pb.counters = L.counters.as<unsigned>();
+      pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
+      pb.segCap = qseg_capacity(pb.capacity);
+      pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
+      // one light: shadow contributions are added by k_trace<true> itself (no resolve pass)
+      pb.fuseShadow = rp.numLights == 1 && !getenv("YRT_NO_SHADOW_FUSE");
+      return pb;
+    };
+    // waits for the lane's previous batch and accounts its queue counters
+    int64_t tilesDone = 0;
+    auto drain = [&](Lane& L) {
+      if (!L.pending) return;
+      HIP_CHECK(hipStreamSynchronize(L.stream));
       for (int d = 0; d < levels; ++d) {
         double nc = 0, ns = 0;
         for (int k = 0; k < YRT_QSEGS; ++k) {
-          nc += hc[qcounter_index(d, 0, k)];
-          ns += hc[qcounter_index(d, 1, k)];
+          nc += L.hc[qcounter_index(d, 0, k)];
+          ns += L.hc[qcounter_index(d, 1, k)];
         }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           stats.raysClosest += nc;
@@ -348,8 +349,61 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         stats.raysShadow += ns;
         if (d < rp.maxDepth && ns) stats.launchesShadow += 1;
       }
-      status(R, 1, float(first + bi.numPixels / 256) / float(std::max(1, shardTiles)));
+      L.pending = false;
+      tilesDone += L.pendTiles;
+      status(R, 1, float(tilesDone) / float(std::max(1, shardTiles)));
+    };
+
+    struct EvPair { hipEvent_t a, b; int kind; };
+    std::vector<EvPair> evs;
+    int64_t batch = 0;
+    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
+      if (R.stopFlag && R.stopFlag->load()) break;
+      Lane& L = lanes[batch % nl];
+      drain(L);
+      const hipStream_t st = L.stream;
+      const PathBuffers pb = lane_buffers(L);
+      SceneView lsv = sv;
+      lsv.traceSpill = L.spill.as<int>();
+      BatchInfo bi;
+      bi.firstTile = (int)first;
+      bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
+      bi.tileStride = shardCount;
+      bi.tileOffset = shardIndex;
+      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
+      launch_raygen(fv, pb, bi, st);
+      for (int d = 0; d < rp.maxDepth; ++d) {
+        const int cur = d & 1;
+        EvPair e1{};
+        if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
+        launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
+                             pb.segCap, pb.hit, st);
+        if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
+        if (captureMax > 0 && first == 0)
+          capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap, st);
+        EvPair e2{};
+        if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
+        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
+        if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
+        if (rp.numLights > 0) {
+          EvPair e3{};
+          if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
+          const ShadowFuse sf{pb.sContrib, pb.pathL};
+          launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
+                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr);
+          if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
+          if (captureMax > 0 && first == 0)
+            capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap, st);
+          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, st);
+        }
+      }
+      launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
+                            dAccu.as<float4>(), accumulate ? 1 : 0, st);
+      HIP_CHECK(hipMemcpyAsync(L.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      L.pending = true;
+      L.pendTiles = bi.numPixels / 256;
     }
+    for (int l = 0; l < nl; ++l) drain(lanes[l]);
     for (auto& e : evs) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));
@@ -361,7 +415,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     eventPool.clear();
     R.iteration++;
   }
-  HIP_CHECK(hipStreamSynchronize(stream));
+  for (int l = 0; l < kMaxLanes; ++l) HIP_CHECK(hipStreamSynchronize(lanes[l].stream));
 
   // framebuffer write-back (api/framebuffer.h:93-226)
   void* dst = F.buffer(F.cur);
