@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
     p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
+    p.add_argument("--stereo-frames", type=int, default=1,
+                   help="C4 stereo cubemaps (12 x 1536^2 x 256spp, tile split over the ranks) timed after the "
+                        "main loop and reported under 'stereo_cubemap' (0: skip)")
     return p.parse_args()
 
 
@@ -166,6 +169,8 @@ def main():
     rays, closest, shadow = tot.tolist()
     elapsed = tmax.item()
 
+    stereo = stereo_cubemap(a, dev, rank, world, backend) if a.stereo_frames > 0 else None
+
     if rank == 0:
         # dominant trace kernel and its roofline (algorithmic bytes / kernel time)
         kern = {
@@ -219,12 +224,65 @@ def main():
             "rays_closest": closest, "rays_shadow": shadow,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "stereo_cubemap": stereo,
         }
         print(json.dumps(out), flush=True)
     ses.close()
     dev.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def stereo_cubemap(a, dev, rank, world, backend):
+    """BASELINE.json configs[3]: the test_stereo stereo cubemap (12 faces x 1536^2, 256 spp,
+    depth 10, test_stereo_view.ecs), every face's 16x16 tiles dealt round-robin over the
+    ranks, the faceCamera billboard refit per face, and one RCCL reduce of the
+    12 RGB8 faces (disjoint tiles) to rank 0 at the end. Strong scaling: the cubemap is the
+    same at every N; Mrays/s = closest + shadow queries of all ranks / max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    import yrt
+    scenes = ROOT / "scenes"
+    ses = yrt.Session(["-i", str(scenes / "test_stereo.xml"), "-c", str(scenes / "test_stereo_view.ecs"),
+                       "-size", "1536", "1536", "-spp", "256", "-stereo"], device=dev)
+    dev.set_tile_shard(rank, world)
+    info = ses.info()
+    W, H = info["width"], info["height"]
+    stride = (3 * W + 3) // 4 * 4
+    faces = torch.zeros((12, stride * H), dtype=torch.uint8, device="cuda" if backend == "nccl" else "cpu")
+    ses.render(0)  # untimed: allocations, sample table
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    rays = 0.0
+    t0 = time.perf_counter()
+    for _ in range(a.stereo_frames):
+        for f in range(12):
+            img = ses.render(f)
+            st = dev.render_stats()
+            rays += st["raysClosest"] + st["raysShadow"]
+            faces[f, :img.size].copy_(torch.from_numpy(np.ascontiguousarray(img).reshape(-1)))
+        if world > 1:
+            dist.reduce(faces, dst=0, op=dist.ReduceOp.SUM)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    red = "cuda" if backend == "nccl" else "cpu"
+    tot = torch.tensor([rays], dtype=torch.float64, device=red)
+    tm = torch.tensor([dt], dtype=torch.float64, device=red)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    ses.close()
+    dev.set_tile_shard(0, 1)
+    dt = tm.item()
+    samples = 12.0 * W * H * 256 * a.stereo_frames
+    return {"metric": "Mrays/s (test_stereo stereo cubemap 12x1536^2 256spp, closest+shadow queries)",
+            "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": world,
+            "scaling": "strong", "ms_per_cubemap": round(dt / a.stereo_frames * 1e3, 1),
+            "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
+            "parallelism": f"face-tiles-roundrobin{world}"}
 
 
 def cpu_baseline(ses, a):
