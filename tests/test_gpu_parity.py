@@ -131,6 +131,20 @@ def test_c3_standin_parity(gpu_device):
     parity(img, ref, 0.995, mad_rel=1e-3)
 
 
+def test_c3_full_size_band_parity(gpu_device):
+    """C3 at its BASELINE size (2048^2, 64 spp, depth 10, 64 M-path batches over two lanes):
+    the GPU frame against the oracle on a centred band of 8 full rows (same frame blob)."""
+    s = _session(gpu_device, c3_args(2048, 64))
+    info = s.info()
+    img = s.render()
+    y0 = 1020
+    ref, _ = oracle.render(s.export_frame(), 2048, 2048, info["gamma"], rect=(0, y0, 2048, y0 + 8),
+                           threads=min(16, oracle.cpu_count()))
+    parity(img[y0:y0 + 8], ref[y0:y0 + 8], 0.995, mad_rel=1e-3)
+    assert np.isfinite(img).all()
+    s.close()
+
+
 @pytest.mark.parametrize("face", [0, 3, 7, 10])
 def test_c4_stereo_face_parity(gpu_device, face):
     img, ref, _ = _render_pair(gpu_device, c4_args(96, 4), face=face)
@@ -158,11 +172,25 @@ def test_tile_shards_compose_bit_exact(gpu_device):
 def test_batch_capacity_invariance(gpu_device):
     s = _session(gpu_device, c2_args(160, 4))
     a = s.render()
-    gpu_device.set_batch_capacity(256 * 4 * 3)  # 3 tiles per wavefront batch
+    gpu_device.set_batch_capacity(256 * 4 * 3)  # 3 tiles per wavefront batch (34 batches, both lanes)
     b = s.render()
-    gpu_device.set_batch_capacity(16 << 20)
+    gpu_device.set_batch_capacity(64 << 20)
     assert np.array_equal(a, b)
     s.close()
+
+
+def test_lanes_invariance(monkeypatch):
+    """Batches spread over one or two lanes (streams) give bit-identical frames."""
+    imgs = []
+    for lanes in ("1", "2"):
+        monkeypatch.setenv("YRT_LANES", lanes)
+        d = yrt.Device(0)
+        d.set_batch_capacity(256 * 4 * 5)
+        s = _session(d, c2_args(160, 4))
+        imgs.append(s.render())
+        s.close()
+        d.close()
+    assert np.array_equal(imgs[0], imgs[1])
 
 
 def test_rgb8_framebuffer_quantization(gpu_device):
