@@ -301,7 +301,10 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_NODE_LOOP 1  // +1.5 % on C3 (node steps chained without the refill block)
 #endif
 #ifndef YRT_TRACE_WAVES
-#define YRT_TRACE_WAVES 6
+#define YRT_TRACE_WAVES 5  // with sign-ordered planes (88 VGPRs); 6 waves cap both kernels at 80
+#endif
+#ifndef YRT_TRACE_WAVES_ANY
+#define YRT_TRACE_WAVES_ANY YRT_TRACE_WAVES  // occupancy target of the shadow-ray instantiation
 #endif
 // A finished shadow query: the occlusion flag, or (fused, PathBuffers::fuseShadow) the
 // light's contribution added to its path's radiance when unoccluded (k_shadow_resolve order).
@@ -320,7 +323,7 @@ __device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restric
 }
 
 template <bool ANY>
-__global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_TRACE_WAVES))) void k_trace(
+__global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
@@ -458,10 +461,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         float t[4];
         int c[4];
 #ifndef YRT_ORDERED_PLANES
-// 2 (default): ordered planes for shadow rays only — k_trace<true> -2.5%, while in
-// k_trace<false> the six per-lane plane addresses cost more than the min/max they save
-// (+11%, 80 VGPRs); 1 = both, 0 = neither
-#define YRT_ORDERED_PLANES 2
+// 1 (default): sign-ordered planes in both kernels, at 5 waves/SIMD (+1.5% on C3 with two
+// lanes); at 6 waves the closest-hit kernel's six per-lane plane addresses pushed it to the
+// 80-VGPR cap and it ran 11% slower. 2 = shadow rays only, 0 = neither
+#define YRT_ORDERED_PLANES 1
 #endif
         if (YRT_ORDERED_PLANES == 1 || (YRT_ORDERED_PLANES == 2 && ANY))
           box4_ordered(nodes + curIdx, r, __float_as_int(ri.w), best.t, t, c);
