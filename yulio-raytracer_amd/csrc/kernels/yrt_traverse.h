@@ -30,7 +30,9 @@
 #define YRT_LDS_STACK 32     // top entries kept in LDS; deeper ones spill (power of two)
 #endif
 static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
+#ifndef YRT_TRACE_BLOCK
 #define YRT_TRACE_BLOCK 128
+#endif
 
 namespace yrt {
 
