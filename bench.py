@@ -47,9 +47,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
     p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
-    p.add_argument("--stereo-frames", type=int, default=1,
+    p.add_argument("--stereo-frames", type=int, default=0,
                    help="C4 stereo cubemaps (12 x 1536^2 x 256spp, tile split over the ranks) timed after the "
-                        "main loop and reported under 'stereo_cubemap' (0: skip)")
+                        "main loop and reported under 'stereo_cubemap'. Off by default so a rocprof summary "
+                        "of the default command averages only the C3 launches of the roofline kernel")
     return p.parse_args()
 
 
