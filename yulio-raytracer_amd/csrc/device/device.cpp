@@ -15,6 +15,8 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <memory>
+#include <deque>
 
 #include "../kernels/yrt_kernels.h"
 #include "image_io.h"
@@ -96,7 +98,11 @@ class Device {
   static constexpr int kMaxLanes = 2;
   Lane lanes[kMaxLanes];
   int numLanes = kMaxLanes;
-  FrameCache fcache;
+  // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
+  // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
+  static constexpr size_t kMaxFrameCaches = 16;
+  std::map<std::string, std::unique_ptr<FrameCache>> fcaches;
+  std::deque<std::string> fcacheOrder;
   std::vector<hipEvent_t> eventPool;
 
   bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
@@ -234,14 +240,23 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
   rp.firstScatterSampleID = 1;
   rp.firstScatterTypeSampleID = 0;
   char keybuf[256];
-  snprintf(keybuf, sizeof(keybuf), "%d/%d/%d/%d/%d/%s/%p", req.spp, req.sets, req.iteration, req.num1D, req.num2D,
-           req.filter.c_str(), (void*)&G);
-  if (fcache.key != keybuf) {
-    build_sample_table(req, fcache.table);
-    fcache.dims.upload(fcache.table.dims);
-    fcache.light.upload(fcache.table.light);
-    fcache.key = keybuf;
+  snprintf(keybuf, sizeof(keybuf), "%d/%d/%d/%d/%d/%s/%llu", req.spp, req.sets, req.iteration, req.num1D, req.num2D,
+           req.filter.c_str(), (unsigned long long)G.serial);
+  auto fit = fcaches.find(keybuf);
+  if (fit == fcaches.end()) {
+    if (fcaches.size() >= kMaxFrameCaches) {
+      fcaches.erase(fcacheOrder.front());
+      fcacheOrder.pop_front();
+    }
+    auto fc = std::make_unique<FrameCache>();
+    build_sample_table(req, fc->table);
+    fc->dims.upload(fc->table.dims);
+    fc->light.upload(fc->table.light);
+    fc->key = keybuf;
+    fcacheOrder.push_back(keybuf);
+    fit = fcaches.emplace(keybuf, std::move(fc)).first;
   }
+  FrameCache& fcache = *fit->second;
   const SampleTable& tab = fcache.table;
   rp.spp = tab.spp;
   rp.sets = tab.sets;

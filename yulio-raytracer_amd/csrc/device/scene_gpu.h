@@ -6,6 +6,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "../kernels/yrt_kernels.h"
@@ -52,6 +53,11 @@ struct DevBuf {
 
 struct GpuScene {
   int device = 0;
+  uint64_t serial = next_serial();  // identifies the committed scene in caches (addresses get reused)
+  static uint64_t next_serial() {
+    static std::atomic<uint64_t> n{1};
+    return n++;
+  }
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels,
       lights, envLights, hdriDist, media;
   SceneView view{};
