@@ -7,7 +7,7 @@
 //    GpuNode  128 B  the four children's AABBs as planes [axis lo/hi][child] (so a packed
 //                    op tests two children's planes at once) + four child references
 //                    (index << 5 | count: count 0 = inner node, 1..31 = leaf triangle
-//                    range, -1 = empty slot).
+//                    range, -1 = empty slot; an empty slot's box is inverted, lo = +inf, hi = -inf).
 //    GpuTri    48 B  Embree-convention Moeller-Trumbore triangle in leaf order:
 //                    v0, e1 = v0-v1, e2 = v2-v0 (rtcore triangle convention);
 //                    v0.w = global triangle id (int bits), e1.w = flags (cull bit).

@@ -477,11 +477,15 @@ struct Collapser {
     }
     GpuNode& g = out[ni];
     memset(&g, 0, sizeof(g));
+    // empty slots get an inverted infinite box (lo = +inf, hi = -inf): with sign-ordered slab
+    // planes its entry distance is +inf and its exit -inf for every ray, so the kernel culls
+    // it without testing the child reference (which stays -1 for the other traversals)
     for (int j = 0; j < 4; ++j) {
       const bool v = j < k;
-      g.lox[j] = v ? ch[j].b.lo[0] : 0.f; g.hix[j] = v ? ch[j].b.hi[0] : 0.f;
-      g.loy[j] = v ? ch[j].b.lo[1] : 0.f; g.hiy[j] = v ? ch[j].b.hi[1] : 0.f;
-      g.loz[j] = v ? ch[j].b.lo[2] : 0.f; g.hiz[j] = v ? ch[j].b.hi[2] : 0.f;
+      const float L = INFINITY, H = -INFINITY;
+      g.lox[j] = v ? ch[j].b.lo[0] : L; g.hix[j] = v ? ch[j].b.hi[0] : H;
+      g.loy[j] = v ? ch[j].b.lo[1] : L; g.hiy[j] = v ? ch[j].b.hi[1] : H;
+      g.loz[j] = v ? ch[j].b.lo[2] : L; g.hiz[j] = v ? ch[j].b.hi[2] : H;
       g.child[j] = refs[j];
     }
     return ni;

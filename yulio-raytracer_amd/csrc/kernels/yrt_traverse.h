@@ -95,6 +95,11 @@ __device__ __forceinline__ int plane_offsets(float ix, float iy, float iz) {
   return ((__float_as_uint(ix) >> 27) & 16) | ((__float_as_uint(iy) >> 19) & (16 << 8)) |
          ((__float_as_uint(iz) >> 11) & (16 << 16));
 }
+// YRT_EMPTY_INF: empty slots carry inverted infinite boxes (device/bvh_build.cpp), which the
+// ordered-plane test culls by itself — the child-reference check is skipped.
+#ifndef YRT_EMPTY_INF
+#define YRT_EMPTY_INF 1
+#endif
 __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, const RayPre& r, int planeOff,
                                              float tmax, float t[4], int c[4]) {
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -117,7 +122,7 @@ __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, con
   do {                                                                           \
     const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                   \
     const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                      \
-    t[k] = ((nn <= ff * YRT_BOX_ROBUST) && (CH) != -1) ? nn : INF;               \
+    t[k] = (nn <= ff * YRT_BOX_ROBUST && (YRT_EMPTY_INF || (CH) != -1)) ? nn : INF; \
     c[k] = (CH);                                                                 \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
