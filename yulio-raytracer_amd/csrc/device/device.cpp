@@ -298,6 +298,13 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     capShadow.clear();
     const int spp = rp.spp;
     int64_t tilesPerBatch = std::max<int64_t>(1, capacity / (256ll * spp));
+    // a multiple of the lanes in batches (evenly sized), so both lanes have work even when a
+    // shard of the frame fits one batch (multi-GPU shards, small frames)
+    if (captureMax == 0 && numLanes > 1 && shardTiles > 1) {
+      int64_t nb = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
+      nb = (nb + numLanes - 1) / numLanes * numLanes;
+      tilesPerBatch = (shardTiles + nb - 1) / nb;
+    }
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
     const int64_t numBatches = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
