@@ -1307,7 +1307,10 @@ static const unsigned kShadeVariants[] = {YRT_SV_UBER, YRT_SV_OBJ, YRT_SV_SPHERE
 template <unsigned MM>
 static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
                            int depth, hipStream_t s) {
-  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, sv, fv, pb,
+#ifndef YRT_SHADE_GRID
+#define YRT_SHADE_GRID 4096  // 2048..32768 swept with two lanes: 4096 +0.4 % over 8192
+#endif
+  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_SHADE_GRID)), dim3(YRT_BLOCK), 0, s, sv, fv, pb,
                      bi, depth);
 }
 
