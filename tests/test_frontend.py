@@ -102,3 +102,26 @@ def test_startrt_writes_cubemap_jpeg(tmp_path):
     # strip segments L,R,U,D,B,F per eye: U and D (2,3 / 8,9) carry no watermark
     assert all(diff[k] > 0 for k in (0, 1, 4, 5, 6, 7, 10, 11)), diff
     assert all(diff[k] <= 2 for k in (2, 3, 8, 9)), diff
+
+
+@pytest.mark.gpu
+def test_stoprt_cancels_a_running_render(tmp_path):
+    """StopRT during a long StartRT (default ParamsRT: 1536^2 faces, 256 spp): a second
+    StartRT is refused with RenderingIsInProgress, the stop flag ends the render at the next
+    wavefront batch, the state becomes Stopped and, keepResults = false, no image is left
+    (renderer.cpp:724-731, 1606-1641)."""
+    import time
+    for f in ("cornell_box.ecs", "cornell_box.obj", "cornell_box.mtl"):
+        shutil.copy(SCENES / f, tmp_path / f)
+    p = yrt.InitParamsRT()
+    assert yrt.StartRT(tmp_path / "cornell_box.ecs", p)
+    assert not yrt.StartRT(tmp_path / "cornell_box.ecs", p)
+    assert yrt.GetLastErrorRT() == 1  # RenderingIsInProgress
+    time.sleep(1.0)
+    t0 = time.time()
+    assert yrt.StopRT(False)
+    assert time.time() - t0 < 60
+    st = yrt.GetCurrentStatusRT()
+    assert st.state == 3  # Stopped
+    assert not (tmp_path / "cornell_box_cubemap.jpg").exists()
+    assert not yrt.WaitRT()  # nothing left to wait for
