@@ -292,7 +292,7 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_PROF(i, v) ((void)0)
 #endif
 #ifndef YRT_TRI_STEP
-#define YRT_TRI_STEP 0
+#define YRT_TRI_STEP 2  // triangles per lane per leaf step (0 = whole leaf): 2 is +0.7 % over whole leaves
 #endif
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 6  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
@@ -533,8 +533,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 #endif
       bool found = false;
 #if YRT_TRI_STEP
-      // one triangle per lane per leaf step: no intra-leaf divergence
-      const int lTake = lCnt > 0 ? 1 : 0;
+      // at most YRT_TRI_STEP triangles per lane per leaf step (the rest of the leaf stays
+      // current / parked): less intra-leaf divergence
+      const int lTake = min(lCnt, YRT_TRI_STEP);
 #else
       const int lTake = lCnt;
 #endif
@@ -559,11 +560,11 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 #if YRT_TRI_STEP
       if (lCnt > 0) {
         if (usePend) {
-          pendIdx += 1;
-          pendCnt -= 1;
-        } else if (curCnt > 1) {
-          curIdx += 1;
-          curCnt -= 1;
+          pendIdx += lTake;
+          pendCnt -= lTake;
+        } else if (curCnt > lTake) {
+          curIdx += lTake;
+          curCnt -= lTake;
         } else {
           YRT_POP();
         }
