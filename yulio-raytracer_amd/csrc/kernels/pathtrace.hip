@@ -522,9 +522,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       const int lCnt = !has ? 0 : usePend ? pendCnt : (curCnt > 0 ? curCnt : 0);
 #ifdef YRT_PROFILE
       {
-        int mx = lCnt;
+        const int lc_ = YRT_TRI_STEP ? min(lCnt, YRT_TRI_STEP) : lCnt;  // triangles this step
+        int mx = lc_;
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-        int sm = lCnt;
+        int sm = lc_;
         for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
         YRT_PROF(4, mx > 0 ? 1 : 0);
         YRT_PROF(5, mx);
