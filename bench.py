@@ -33,7 +33,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md §HBM
-NODE_BYTES, TRI_BYTES = 128, 48  # GpuNode (4-wide) / GpuTri (csrc/common/yrt_gpu_types.h)
+NODE_BYTES = 128  # GpuNode (4-wide); triangle record bytes from the scene (GpuTri, 48 or 64)
 
 
 def parse():
@@ -101,7 +101,8 @@ def main():
         for depth in range(64):
             org, dr, total = dev.captured_rays(shadow, depth)
             if len(org):
-                nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow))
+                nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow),
+                                                tri_bytes=sinfo["triRecordBytes"])
                 tot_rays += total
                 tot_nodes += nv / len(org) * total
                 tot_tris += tv / len(org) * total
@@ -110,7 +111,7 @@ def main():
         io = 32 + (4 if shadow else 16)
         per_kind["shadow" if shadow else "closest"] = {
             "nodes_per_ray": n_node, "tris_per_ray": n_tri,
-            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * TRI_BYTES}
+            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * sinfo["triRecordBytes"]}
 
     # ---- warmup + timed frames
     dev.set_kernel_timing(True)

@@ -155,6 +155,7 @@ typedef struct YRTSceneInfo {
   double buildSeconds;
   float bboxLo[3], bboxHi[3];
   int64_t numTriRefs;
+  int64_t triRecordBytes;  /* bytes per leaf triangle record (48, or 64 with a stored normal) */
 } YRTSceneInfo;
 YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
 /* Copies the host mirror of the BVH (4-wide nodes: 128 B each, numTriRefs leaf tris: 48 B each). */

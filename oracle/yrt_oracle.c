@@ -2209,9 +2209,10 @@ int oracle_scene_triangles(const void* blob, size_t bytes, float* out, int maxTr
 typedef struct { float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4]; int32_t child[4], pad[4]; } DNode;
 typedef struct { float v0[4], e1[4], e2[4]; } DTri;
 int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, size_t numTris, const float* org4,
-                        const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4) {
+                        const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
+                        size_t triStride /* bytes per leaf record: 48, or 64 with a stored normal */) {
   const DNode* nodes = (const DNode*)nodes_;
-  const DTri* tris = (const DTri*)tris_;
+  const char* trisBytes = (const char*)tris_;
   (void)numNodes; (void)numTris;
   double nv = 0, tv = 0;
   const float INF = (float)INFINITY;
@@ -2259,7 +2260,7 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
         } else {
           const int ci = cur >> 5, cc = cur & 31;
           for (int k = 0; k < cc; ++k) {
-            const DTri* t = &tris[ci + k];
+            const DTri* t = (const DTri*)(trisBytes + (size_t)(ci + k) * triStride);
             tv += 1;
             uint32_t fl;
             int gid;

@@ -67,7 +67,8 @@ int oracle_trace(const void* blob, size_t bytes, const float* org4, const float*
  * algorithmic bytes. */
 int oracle_count_visits(const void* nodes, size_t numNodes, const void* tris, size_t numTris, const float* org4,
                         const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits,
-                        float* hit4);
+                        float* hit4,
+                        size_t triStride);
 
 /* Reference Random (common/math/random.h): n draws of getInt() after setSeed(seed). */
 void oracle_random_ints(int seed, int n, int32_t* out);

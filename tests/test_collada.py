@@ -65,7 +65,8 @@ def test_dae_culling_modes(host_device, tmp_path, mode, culled):
     s = _session(host_device, f, "-faceCullingMode", mode) if mode == "default" else \
         yrt.Session(["-fprCollada", "-faceCullingMode", mode, "-i", str(f), "-stereo"], device=host_device)
     _, tris = host_device.export_bvh(s.info()["scene"])
-    flags = tris.view(np.uint32).reshape(-1, 12)[:, 7]
+    rec = host_device.scene_info(s.info()["scene"])["triRecordBytes"] // 4
+    flags = tris.view(np.uint32).reshape(-1, rec)[:, 7]
     assert int((flags & 1).sum()) == culled
     s.close()
 
@@ -172,7 +173,8 @@ def test_face_camera_refit_equals_rebuild(gpu_device, tmp_path):
                 dir_ = np.zeros((n, 4), np.float32)
                 dir_[:, :3] = d / np.linalg.norm(d, axis=1, keepdims=True)
                 dir_[:, 3] = np.inf
-                h_dev = oracle.count_visits(nodes, tris, org, dir_, any_hit=False)[2]
+                h_dev = oracle.count_visits(nodes, tris, org, dir_, any_hit=False,
+                                            tri_bytes=gpu_device.scene_info(scene)["triRecordBytes"])[2]
                 h_ref = oracle.trace(blob, org, dir_)
                 assert np.array_equal(h_dev[:, 3].view(np.int32), h_ref[:, 3].view(np.int32))
             s.close()

@@ -150,7 +150,8 @@ def test_device_bvh_gives_oracle_hits(host_device, which, sbvh, monkeypatch):
     nodes, tris = host_device.export_bvh(scene)
     org4, dir4 = _incoherent(blob, 4096)
     ref = oracle.trace(blob, org4, dir4)
-    nv, tv, hit = oracle.count_visits(nodes, tris, org4, dir4)
+    nv, tv, hit = oracle.count_visits(nodes, tris, org4, dir4,
+                                      tri_bytes=host_device.scene_info(scene)["triRecordBytes"])
     assert np.array_equal(hit[:, 3].view(np.int32), ref[:, 3].view(np.int32))
     m = ref[:, 3].view(np.int32) >= 0
     assert np.array_equal(hit[m, :3], ref[m, :3])

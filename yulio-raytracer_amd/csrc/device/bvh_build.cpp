@@ -577,6 +577,13 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
     g.v0[0] = t[0]; g.v0[1] = t[1]; g.v0[2] = t[2];
     g.e1[0] = t[0] - t[3]; g.e1[1] = t[1] - t[4]; g.e1[2] = t[2] - t[5];
     g.e2[0] = t[6] - t[0]; g.e2[1] = t[7] - t[1]; g.e2[2] = t[8] - t[2];
+#if YRT_TRI_NG
+    // cross(e1, e2) in the device's order (common/yrt_math.h)
+    g.ng[0] = g.e1[1] * g.e2[2] - g.e1[2] * g.e2[1];
+    g.ng[1] = g.e1[2] * g.e2[0] - g.e1[0] * g.e2[2];
+    g.ng[2] = g.e1[0] * g.e2[1] - g.e1[1] * g.e2[0];
+    g.ng[3] = 0.f;
+#endif
     int gid = id;
     uint32_t fl = flags[id];
     memcpy(&g.v0[3], &gid, 4);

@@ -1124,6 +1124,7 @@ int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out) {
   out->numGeometries = S->gpu->numGeoms;
   out->numNodes = (int64_t)S->gpu->hNodes.size();
   out->numTriRefs = (int64_t)S->gpu->hTris.size();
+  out->triRecordBytes = (int64_t)sizeof(GpuTri);
   out->bvhDepth = S->gpu->bvhDepth;
   out->numLights = S->gpu->view.numLights;
   out->buildSeconds = S->gpu->buildSeconds;

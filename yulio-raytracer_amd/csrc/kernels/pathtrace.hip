@@ -1416,6 +1416,11 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ t
     t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z;
     t.e1[0] = a.x - b.x; t.e1[1] = a.y - b.y; t.e1[2] = a.z - b.z;
     t.e2[0] = c.x - a.x; t.e2[1] = c.y - a.y; t.e2[2] = c.z - a.z;
+#if YRT_TRI_NG
+    t.ng[0] = t.e1[1] * t.e2[2] - t.e1[2] * t.e2[1];
+    t.ng[1] = t.e1[2] * t.e2[0] - t.e1[0] * t.e2[2];
+    t.ng[2] = t.e1[0] * t.e2[1] - t.e1[1] * t.e2[0];
+#endif
   }
 }
 

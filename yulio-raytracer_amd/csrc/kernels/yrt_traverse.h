@@ -175,7 +175,11 @@ __device__ __forceinline__ bool tri_test_t(const GpuTri& tr, const RayPre& r, fl
   V3 v0 = v3(tr.v0[0], tr.v0[1], tr.v0[2]);
   V3 e1 = v3(tr.e1[0], tr.e1[1], tr.e1[2]);
   V3 e2 = v3(tr.e2[0], tr.e2[1], tr.e2[2]);
+#if YRT_TRI_NG
+  V3 Ng = v3(tr.ng[0], tr.ng[1], tr.ng[2]);
+#else
   V3 Ng = cross(e1, e2);
+#endif
   V3 C = v0 - r.org;
   V3 R = cross(r.dir, C);
   float den = dot(Ng, r.dir);

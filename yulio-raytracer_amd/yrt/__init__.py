@@ -294,10 +294,11 @@ class Device:
         return d
 
     def export_bvh(self, scene):
-        """Host mirror of the uploaded BVH: (nodes uint8[numNodes*128], tris uint8[numTriRefs*48])."""
+        """Host mirror of the uploaded BVH: (nodes uint8[numNodes*128],
+        tris uint8[numTriRefs*triRecordBytes])."""
         info = self.scene_info(scene)
         nodes = np.zeros(info["numNodes"] * 128, np.uint8)
-        tris = np.zeros(info["numTriRefs"] * 48, np.uint8)
+        tris = np.zeros(info["numTriRefs"] * info["triRecordBytes"], np.uint8)
         self._rc(N.dev.yrtExportBVH(self.h, scene, nodes.ctypes.data, nodes.nbytes, tris.ctypes.data, tris.nbytes),
                  "export_bvh")
         return nodes, tris

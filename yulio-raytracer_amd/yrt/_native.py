@@ -52,7 +52,8 @@ class RenderStats(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("numTriangles", C.c_int64), ("numGeometries", C.c_int64), ("numNodes", C.c_int64),
                 ("bvhDepth", C.c_int64), ("numLights", C.c_int64), ("buildSeconds", C.c_double),
-                ("bboxLo", C.c_float * 3), ("bboxHi", C.c_float * 3), ("numTriRefs", C.c_int64)]
+                ("bboxLo", C.c_float * 3), ("bboxHi", C.c_float * 3), ("numTriRefs", C.c_int64),
+                ("triRecordBytes", C.c_int64)]
 
 
 class SessionInfo(C.Structure):
