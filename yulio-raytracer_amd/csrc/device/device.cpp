@@ -353,6 +353,11 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
       pb.fuseShadow = rp.numLights == 1 && !getenv("YRT_NO_SHADOW_FUSE");
       return pb;
     };
+    // queue lengths of the last drained batch per depth: grid-size hints for the next batches
+    // (batches of one frame see similar queues; -1 = no estimate yet, full grids)
+    std::vector<long long> estClosest(levels, -1), estShadow(levels, -1);
+    const bool useHints = !getenv("YRT_NO_GRID_HINTS");
+    auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + 65536; };
     // waits for the lane's previous batch and accounts its queue counters
     int64_t tilesDone = 0;
     auto drain = [&](Lane& L) {
@@ -364,6 +369,8 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
           nc += L.hc[qcounter_index(d, 0, k)];
           ns += L.hc[qcounter_index(d, 1, k)];
         }
+        estClosest[d] = (long long)nc;
+        estShadow[d] = (long long)ns;
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           stats.raysClosest += nc;
           if (nc) stats.launchesClosest += 1;
@@ -399,24 +406,24 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         EvPair e1{};
         if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
         launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                             pb.segCap, pb.hit, st);
+                             pb.segCap, pb.hit, st, hint(estClosest[d]));
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
           capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap, st);
         EvPair e2{};
         if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
-        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
+        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st, hint(estClosest[d]));
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (rp.numLights > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
           const ShadowFuse sf{pb.sContrib, pb.pathL};
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr);
+                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr, hint(estShadow[d]));
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
             capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap, st);
-          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, st);
+          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, st, hint(estClosest[d]));
         }
       }
       launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,

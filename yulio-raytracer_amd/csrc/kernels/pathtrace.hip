@@ -1279,16 +1279,20 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
   hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
 }
 
+static inline long long hinted(long long maxCount, long long hint) {
+  return hint >= 0 && hint < maxCount ? hint : maxCount;
+}
+
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s) {
-  const long long maxCount = (long long)numSegs * segCap;
+                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint) {
+  const long long maxCount = hinted((long long)numSegs * segCap, countHint);
   hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
                      0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{});
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse) {
-  const long long maxCount = (long long)numSegs * segCap;
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, long long countHint) {
+  const long long maxCount = hinted((long long)numSegs * segCap, countHint);
   hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
                      0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill,
                      fuse ? *fuse : ShadowFuse{});
@@ -1308,16 +1312,17 @@ static const unsigned kShadeVariants[] = {YRT_SV_UBER, YRT_SV_OBJ, YRT_SV_SPHERE
 
 template <unsigned MM>
 static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
-                           int depth, hipStream_t s) {
+                           int depth, hipStream_t s, long long countHint) {
 #ifndef YRT_SHADE_GRID
 #define YRT_SHADE_GRID 4096  // 2048..32768 swept with two lanes: 4096 +0.4 % over 8192
 #endif
-  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_SHADE_GRID)), dim3(YRT_BLOCK), 0, s, sv, fv, pb,
+  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(hinted(pb.capacity, countHint), YRT_BLOCK, YRT_SHADE_GRID)),
+                     dim3(YRT_BLOCK), 0, s, sv, fv, pb,
                      bi, depth);
 }
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  unsigned materialMask, hipStream_t s) {
+                  unsigned materialMask, hipStream_t s, long long countHint) {
   unsigned pick = YRT_SV_ALL;
   for (unsigned v : kShadeVariants)
     if ((materialMask & ~v) == 0) {
@@ -1325,16 +1330,17 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
       break;
     }
   switch (pick) {
-    case YRT_SV_UBER: launch_shade_t<YRT_SV_UBER>(sv, fv, pb, bi, depth, s); break;
-    case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s); break;
-    case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s); break;
-    case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s); break;
-    default: launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_UBER: launch_shade_t<YRT_SV_UBER>(sv, fv, pb, bi, depth, s, countHint); break;
+    case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s, countHint); break;
+    case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s, countHint); break;
+    case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s, countHint); break;
+    default: launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s, countHint); break;
   }
 }
 
-void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {
-  hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, pb, depth,
+void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s, long long countHint) {
+  hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(hinted(pb.capacity, countHint), YRT_BLOCK, 8192)), dim3(YRT_BLOCK),
+                     0, s, pb, depth,
                      numLights);
 }
 

@@ -110,15 +110,18 @@ void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int h
 void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s);
 // counts: first segment counter of the queue (segments YRT_QCSTRIDE apart), numSegs segments
 // of segCap slots; hit/occluded are indexed by physical slot.
+// countHint (>= 0): expected queue length, sizes the grid (the kernels grid-stride over the
+// real device-side count, so a low hint costs speed, never correctness); -1: full grid.
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s);
+                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1);
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr);
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr,
+                      long long countHint = -1);
 // materialMask: bit MAT_x set for every material type the scene uses (selects a specialized
 // instantiation of the shade kernel)
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  unsigned materialMask, hipStream_t s);
-void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
+                  unsigned materialMask, hipStream_t s, long long countHint = -1);
+void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s, long long countHint = -1);
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
