@@ -1278,7 +1278,10 @@ void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int h
 
 void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s) {
   // spp is read on device; the host passes the path count through capacity sizing.
-  hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
+#ifndef YRT_RAYGEN_GRID
+#define YRT_RAYGEN_GRID 16384
+#endif
+  hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_RAYGEN_GRID)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
 }
 
 static inline long long hinted(long long maxCount, long long hint) {
