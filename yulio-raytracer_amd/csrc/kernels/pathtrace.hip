@@ -303,7 +303,10 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_NODE_LOOP 1  // +1.5 % on C3 (node steps chained without the refill block)
 #endif
 #ifndef YRT_TRACE_WAVES
-#define YRT_TRACE_WAVES 5  // with sign-ordered planes (88 VGPRs); 6 waves cap both kernels at 80
+// 6: a scheduling target — the 16 KB LDS stack of a 128-lane block holds the kernels at 5
+// waves/SIMD, but code scheduled for 6 (78/74 VGPRs with SGPR-based node addressing) runs
+// +0.6 % on C3 over code scheduled for 5 (profiles/r01/variants_r01.txt)
+#define YRT_TRACE_WAVES 6
 #endif
 #ifndef YRT_TRACE_WAVES_ANY
 #define YRT_TRACE_WAVES_ANY YRT_TRACE_WAVES  // occupancy target of the shadow-ray instantiation
@@ -324,6 +327,12 @@ __device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restric
   }
 }
 
+#ifndef YRT_QCURSOR
+#define YRT_QCURSOR 0  // wave-uniform segment cursor, LDS 16384 B per block: measured -0.2 % (noise level), off
+#endif
+#if YRT_QCURSOR && defined(YRT_PREFETCH) && YRT_PREFETCH
+#error "YRT_PREFETCH uses the LDS prefix table: build it with YRT_QCURSOR=0"
+#endif
 #ifndef YRT_PREFETCH
 #define YRT_PREFETCH 0  // prefetched refill: -0.3 % at refill 24, -1.2/-2.5/-3.0 % at 16/8/4: off
 #endif
@@ -349,9 +358,18 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
                                                          ShadowFuse sf) {
   __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
+#if YRT_QCURSOR
+  // Wave-uniform cursor over the queue segments instead of a block-wide prefix table in LDS:
+  // the table's 132 bytes put a block over 16 KB and cost a resident block per CU (9 -> 10
+  // blocks of 128 lanes), and a refill's logical -> physical mapping becomes a compare per
+  // segment its range touches (usually one) instead of a 5-step LDS binary search.
+  unsigned n = 0;
+  for (int k = 0; k < numSegs; ++k) n += counts[(size_t)k * YRT_QCSTRIDE];
+#else
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
   const unsigned n = qm.pre[YRT_QSEGS];
+#endif
   const int lane = lane_id();
   const unsigned wavesPerBlock = YRT_TRACE_BLOCK / 64;
   const unsigned gw = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
@@ -361,6 +379,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   unsigned next = gw * chunk;
   const unsigned end = min(n, next + chunk);
   if (next >= end) return;  // wave-uniform
+#if YRT_QCURSOR
+  // [segLo, segHi): logical range of segment seg, the one holding `next`
+  int seg = 0;
+  unsigned segLo = 0, segHi = counts[0];
+  while (segHi <= next) {
+    seg += 1;
+    segLo = segHi;
+    segHi += counts[(size_t)seg * YRT_QCSTRIDE];
+  }
+#endif
 
   const GpuNode* __restrict__ nodes = sv.nodes;
   const GpuTri* __restrict__ tris = sv.tris;
@@ -465,6 +493,23 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             q = q2;
             ro = o2;
             rd = d2;
+#elif YRT_QCURSOR
+        const unsigned li = next + (unsigned)__popcll(idle & ltMask);
+        {
+          // segments covering [next, min(next + nIdle, end)), walked wave-uniformly
+          const unsigned hiLi = min(next + (unsigned)nIdle, end);
+          while (true) {
+            if (!has && li >= segLo && li < segHi) q = seg * segCap + (int)(li - segLo);
+            if (segHi >= hiLi) break;
+            seg += 1;
+            segLo = segHi;
+            segHi += counts[(size_t)seg * YRT_QCSTRIDE];
+          }
+        }
+        if (!has) {
+          if (li < end) {
+            ro = org[q];
+            rd = dir[q];
 #else
         if (!has) {
           const unsigned li = next + (unsigned)__popcll(idle & ltMask);
@@ -532,7 +577,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 #define YRT_ORDERED_PLANES 1
 #endif
         if (YRT_ORDERED_PLANES == 1 || (YRT_ORDERED_PLANES == 2 && ANY))
-          box4_ordered(nodes + curIdx, r, __float_as_int(ri.w), best.t, t, c);
+          box4_ordered(nodes + curIdx, r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
         else
           box4(nodes + curIdx, r, best.t, t, c);
 #ifndef YRT_CHILD_ORDER

@@ -100,15 +100,36 @@ __device__ __forceinline__ int plane_offsets(float ix, float iy, float iz) {
 #ifndef YRT_EMPTY_INF
 #define YRT_EMPTY_INF 1
 #endif
+// YRT_NODE_SADDR: the six plane loads and the child load address the node array as a uniform
+// (SGPR) base plus a 32-bit per-lane byte offset (global_load saddr form) instead of six
+// 64-bit per-lane pointers.
+#ifndef YRT_NODE_SADDR
+#define YRT_NODE_SADDR 1
+#endif
 __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, const RayPre& r, int planeOff,
-                                             float tmax, float t[4], int c[4]) {
+                                             float tmax, float t[4], int c[4], const GpuNode* __restrict__ base,
+                                             int nodeIdx) {
   typedef float f2 __attribute__((ext_vector_type(2)));
+#if YRT_NODE_SADDR
+  (void)np;
+  const char* b0 = (const char*)base;
+  const unsigned nb = (unsigned)nodeIdx << 7;
+  const unsigned ox = (unsigned)planeOff & 0xffu, oy = ((unsigned)planeOff >> 8) & 0xffu,
+                 oz = (unsigned)planeOff >> 16;
+  const float4 nx = *(const float4*)(b0 + (nb + ox)), fx = *(const float4*)(b0 + (nb + (16u - ox)));
+  const float4 ny = *(const float4*)(b0 + (nb + (32u + oy))), fy = *(const float4*)(b0 + (nb + (48u - oy)));
+  const float4 nz = *(const float4*)(b0 + (nb + (64u + oz))), fz = *(const float4*)(b0 + (nb + (80u - oz)));
+  const int4 ch = *(const int4*)(b0 + (nb + 96u));
+#else
+  (void)base;
+  (void)nodeIdx;
   const char* b = (const char*)np;
   const int ox = planeOff & 0xff, oy = (planeOff >> 8) & 0xff, oz = planeOff >> 16;
   const float4 nx = *(const float4*)(b + ox), fx = *(const float4*)(b + (16 - ox));
   const float4 ny = *(const float4*)(b + 32 + oy), fy = *(const float4*)(b + (48 - oy));
   const float4 nz = *(const float4*)(b + 64 + oz), fz = *(const float4*)(b + (80 - oz));
   const int4 ch = *(const int4*)(b + 96);
+#endif
   const f2 ox2 = {r.org.x, r.org.x}, oy2 = {r.org.y, r.org.y}, oz2 = {r.org.z, r.org.z};
   const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
   const f2 nx01 = (f2{nx.x, nx.y} - ox2) * ix, nx23 = (f2{nx.z, nx.w} - ox2) * ix;
