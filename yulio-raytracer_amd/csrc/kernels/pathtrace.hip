@@ -282,7 +282,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 // This keeps 64-wide waves busy although ray costs differ by 10-100x. Same visit order and
 // the same (t, triangle id) closest-hit rule as traverse<>.
 #ifndef YRT_REFILL
-#define YRT_REFILL 24  // re-swept at the 32-entry stack: 24 with node bias 6 +1.3 % over 16/4
+#define YRT_REFILL 28  // 24 with node bias 6: +1.3 % over 16/4; 28 with 64-lane blocks: +0.4 % over 24
 #endif
 #ifdef YRT_PROFILE
 // [0] outer iterations x waves, [1] lanes holding a ray at outer iterations,

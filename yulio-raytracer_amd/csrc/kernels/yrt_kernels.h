@@ -31,7 +31,8 @@ struct SceneView {
   int numLights, numEnvLights, numNodes, numTris;
 };
 
-// Trace grid: 16384 blocks of 128 lanes, several times the resident blocks (256 CUs x ~9),
+// Trace grid: 16384 blocks (swept with 128-lane blocks; with 64-lane blocks 32768 is -0.5 %),
+// several times the resident blocks (256 CUs x ~9),
 // so a CU always has a queued block when one drains and the other lane's kernels interleave
 // (sweep 1024..16384 blocks: 16384 best, +1.2 % over 8192 with the 32-entry LDS stack).
 #ifndef YRT_TRACE_GRID

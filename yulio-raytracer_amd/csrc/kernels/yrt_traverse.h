@@ -13,10 +13,9 @@
 //   closest hit: smallest (t, global triangle id) — order independent, so any BVH gives
 //   the same answer (used to pin the GPU against the oracle's own BVH).
 // Stack: per-lane short stack in LDS, [depth][lane] so a wave's pushes hit 64 distinct
-// banks. Only YRT_LDS_STACK entries live in LDS (32 x 256 B per wave: 16 KB per 128-lane
-// block, so LDS and the 5-waves/SIMD VGPR budget cap occupancy together); deeper entries
-// spill to global memory. 32 entries instead of 16: +4.9 % on C3 (the 16-entry ring spilled
-// often enough to matter).
+// banks. Only YRT_LDS_STACK entries live in LDS (32 x 256 B per wave: 8 KB per 64-lane
+// block, so LDS caps occupancy at 5 waves/SIMD); deeper entries spill to global memory.
+// 32 entries instead of 16: +4.9 % on C3 (the 16-entry ring spilled often enough to matter).
 // The builder bounds the tree depth to YRT_STACK_DEPTH-1 (device/bvh_build.cpp).
 #pragma once
 
@@ -31,7 +30,9 @@
 #endif
 static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
 #ifndef YRT_TRACE_BLOCK
-#define YRT_TRACE_BLOCK 128
+// one wave per block (8 KB of LDS stack): +1.0 % on C3 over 128-lane blocks once the trace code
+// was scheduled for a 6-wave target (profiles/r01/variants_r01.txt)
+#define YRT_TRACE_BLOCK 64
 #endif
 
 namespace yrt {
