@@ -282,7 +282,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 // This keeps 64-wide waves busy although ray costs differ by 10-100x. Same visit order and
 // the same (t, triangle id) closest-hit rule as traverse<>.
 #ifndef YRT_REFILL
-#define YRT_REFILL 28  // 24 with node bias 6: +1.3 % over 16/4; 28 with 64-lane blocks: +0.4 % over 24
+#define YRT_REFILL 40  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6
 #endif
 #ifdef YRT_PROFILE
 // [0] outer iterations x waves, [1] lanes holding a ray at outer iterations,
@@ -297,7 +297,7 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_TRI_STEP 2  // triangles per lane per leaf step (0 = whole leaf): 2 is +0.7 % over whole leaves
 #endif
 #ifndef YRT_NODE_BIAS
-#define YRT_NODE_BIAS 6  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
+#define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
 #ifndef YRT_NODE_LOOP
 #define YRT_NODE_LOOP 1  // +1.5 % on C3 (node steps chained without the refill block)
