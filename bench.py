@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--spp", type=int, default=64)
     p.add_argument("--cpu-rows", type=int, default=112, help="rows of the centred CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--capture", type=int, default=4096, help="rays per depth sampled for visit counts")
+    p.add_argument("--capture", type=int, default=4096,
+                   help="rays per depth sampled for visit counts (0: no capture frame, e.g. PMC passes)")
     p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
     p.add_argument("--stereo-frames", type=int, default=0,
                    help="C4 stereo cubemaps (12 x 1536^2 x 256spp, tile split over the ranks) timed after the "
@@ -90,28 +91,9 @@ def main():
         dev.set_batch_capacity(a.capacity)
 
     # ---- untimed capture frame: visit counts of the real query streams (roofline bytes)
-    import oracle
-    dev.set_ray_capture(a.capture)
-    dev.rtRenderFrame(R, cam, S, T, F, 0)
-    dev.set_ray_capture(0)
-    nodes, tris = dev.export_bvh(S)
     per_kind = {}
-    for shadow in (0, 1):
-        tot_rays = tot_nodes = tot_tris = 0.0
-        for depth in range(64):
-            org, dr, total = dev.captured_rays(shadow, depth)
-            if len(org):
-                nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow),
-                                                tri_bytes=sinfo["triRecordBytes"])
-                tot_rays += total
-                tot_nodes += nv / len(org) * total
-                tot_tris += tv / len(org) * total
-        n_node = tot_nodes / max(tot_rays, 1)
-        n_tri = tot_tris / max(tot_rays, 1)
-        io = 32 + (4 if shadow else 16)
-        per_kind["shadow" if shadow else "closest"] = {
-            "nodes_per_ray": n_node, "tris_per_ray": n_tri,
-            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * sinfo["triRecordBytes"]}
+    if a.capture > 0:
+        per_kind = visit_counts(a, dev, R, cam, S, T, F, sinfo)
 
     # ---- warmup + timed frames
     dev.set_kernel_timing(True)
@@ -174,31 +156,40 @@ def main():
     stereo = stereo_cubemap(a, dev, rank, world, backend) if a.stereo_frames > 0 else None
 
     if rank == 0:
-        # dominant trace kernel and its roofline (algorithmic bytes / kernel time)
+        # dominant trace kernel: what binds it. The BVH and the
+        # triangles are L2/MALL-resident, so the traversal is not HBM-bound: the roofline is
+        # the VALU-issue one (PMC pass of this same config, profiles/pmc_c3.json), with the
+        # counter-measured HBM bytes beside it; the SURVEY §8(d) algorithmic bytes are
+        # reported as what they are (mostly L2/MALL hits), never as an HBM rate.
         kern = {
             "closest": (acc["msClosest"], acc["closest"], acc["nClosest"]),
             "shadow": (acc["msShadow"], acc["shadow"], acc["nShadow"]),
         }
         dom = max(kern, key=lambda k: kern[k][0])
         ms, nr, nl = kern[dom]
-        bytes_total = nr * per_kind[dom]["bytes_per_ray"]
-        achieved = bytes_total / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        # HBM bytes per launch of the same kernel from the committed PMC pass on this workload
-        # (tools/gpu_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM)
-        traffic = None
-        tf = ROOT / "profiles" / "traffic.json"
+        avg_ms = ms / max(nl, 1)
         kname = "k_trace<false>" if dom == "closest" else "k_trace<true>"
-        if tf.exists():
-            try:
-                traffic = round(json.loads(tf.read_text())["kernels"][kname]["hbm_bytes_per_dispatch"])
-            except (KeyError, ValueError):
-                traffic = None
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": "profiles/traffic.json (rocprofv3 PMC, same workload)" if traffic else None,
+        alg = nr * per_kind[dom]["bytes_per_ray"] / max(nl, 1) if per_kind else None
+        pmc, pmc_note = load_pmc(a, sinfo, world)
+        kp = (pmc or {}).get("kernels", {}).get(kname, {})
+        traffic = kp.get("hbm_bytes_per_dispatch")
+        valu = kp.get("valu_busy")
+        hbm_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic and avg_ms > 0 else None
+        roof = {"bound": "valu-issue", "achieved": round(valu, 4) if valu is not None else None, "peak": 1.0,
+                "unit": "VALU-busy fraction of SIMD cycles",
+                "frac": round(valu, 4) if valu is not None else None,
+                "traffic": round(traffic) if traffic else None,
                 "kernel": "k_trace_closest" if dom == "closest" else "k_trace_any",
-                "launches": int(nl), "avg_launch_ms": round(ms / max(nl, 1), 4),
-                "algorithmic_bytes_per_launch": round(bytes_total / max(nl, 1)),
+                "launches": int(nl), "avg_launch_ms": round(avg_ms, 4),
+                "valu_ceiling": (pmc or {}).get("calibration", {}).get("valu_busy") if pmc else None,
+                "valu_ceiling_note": "the same formula on a pure-FMA kernel at 8 waves/SIMD (tools/valu_calib.hip)",
+                "hbm": {"achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
+                        "bytes_per_launch": round(traffic) if traffic else None},
+                "algorithmic_bytes_per_launch": round(alg) if alg else None,
+                "algorithmic_note": "SURVEY 8(d) bytes (ray+hit+N_node*128+N_tri*48); node/triangle reads are "
+                                    "L2/MALL hits, so this is not an HBM rate",
+                "pmc_source": pmc_note,
                 "visits": per_kind,
                 "kernel_ms_per_step": {"trace_closest": acc["msClosest"] / a.steps,
                                        "trace_shadow": acc["msShadow"] / a.steps,
@@ -207,7 +198,7 @@ def main():
         if not a.no_cpu_baseline:
             cpu = cpu_baseline(ses, a)
         out = {
-            "metric": "Mrays/s (Sponza stand-in 2048^2 64spp, closest+shadow queries)",
+            "metric": f"Mrays/s (Sponza stand-in {a.size}^2 {a.spp}spp, closest+shadow queries)",
             "value": round(rays / elapsed / 1e6, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -219,9 +210,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural Sponza-class atrium, seed 1234; Sponza.DAE absent)",
-            "config": {"workload": "C3 sponza_standin 2048x2048 64spp depth10 dome(8,8,8) tMaxShadowRay120",
-                       "width": a.size, "height": a.size, "spp": a.spp, "triangles": sinfo["numTriangles"],
-                       "bvh_nodes": sinfo["numNodes"], "parallelism": f"tiles-roundrobin{world}"},
+            "config": workload_config(a, sinfo, world),
             "samples_per_s": round(samples_total / elapsed, 1),
             "rays_closest": closest, "rays_shadow": shadow,
             "roofline": roof,
@@ -233,6 +222,86 @@ def main():
     dev.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def workload_config(a, sinfo, world):
+    """config.workload built from the run's own arguments (C3 only at its BASELINE size)."""
+    c3 = a.size == 2048 and a.spp == 64
+    name = "C3" if c3 else "C3-reduced"
+    return {"workload": f"{name} sponza_standin {a.size}x{a.size} {a.spp}spp depth10 dome(8,8,8) tMaxShadowRay120",
+            "width": a.size, "height": a.size, "spp": a.spp, "triangles": sinfo["numTriangles"],
+            "bvh_nodes": sinfo["numNodes"], "batch_capacity": a.capacity or "default",
+            "parallelism": f"tiles-roundrobin{world}"}
+
+
+def visit_counts(a, dev, R, cam, S, T, F, sinfo):
+    """Untimed capture frame: node/triangle visits per query of the real query streams (a
+    strided sample per depth, counted by the oracle's restatement of this traversal) for the
+    SURVEY §8(d) algorithmic bytes."""
+    import oracle
+    dev.set_ray_capture(a.capture)
+    dev.rtRenderFrame(R, cam, S, T, F, 0)
+    dev.set_ray_capture(0)
+    nodes, tris = dev.export_bvh(S)
+    per_kind = {}
+    for shadow in (0, 1):
+        tot_rays = tot_nodes = tot_tris = 0.0
+        for depth in range(64):
+            org, dr, total = dev.captured_rays(shadow, depth)
+            if len(org):
+                nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow),
+                                                tri_bytes=sinfo["triRecordBytes"])
+                tot_rays += total
+                tot_nodes += nv / len(org) * total
+                tot_tris += tv / len(org) * total
+        n_node = tot_nodes / max(tot_rays, 1)
+        n_tri = tot_tris / max(tot_rays, 1)
+        io = 32 + (4 if shadow else 16)
+        per_kind["shadow" if shadow else "closest"] = {
+            "nodes_per_ray": n_node, "tris_per_ray": n_tri,
+            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * sinfo["triRecordBytes"]}
+    return per_kind
+
+
+def load_pmc(a, sinfo, world):
+    """PMC counters of this same workload (tools/gpu_pmc.sh -> tools/pmc_json.py ->
+    profiles/pmc_c3.json). Used only when the recorded config equals this run's; else null."""
+    f = ROOT / "profiles" / "pmc_c3.json"
+    if not f.exists():
+        return None, "no profiles/pmc_c3.json"
+    try:
+        pmc = json.loads(f.read_text())
+    except ValueError:
+        return None, "unreadable profiles/pmc_c3.json"
+    want = workload_config(a, sinfo, world)
+    got = pmc.get("config", {})
+    keys = ("width", "height", "spp", "triangles", "bvh_nodes", "batch_capacity")
+    if any(got.get(k) != want[k] for k in keys) or world != 1:
+        return None, "profiles/pmc_c3.json was collected on another config: " + json.dumps({k: got.get(k) for k in keys})
+    return pmc, f"profiles/pmc_c3.json ({pmc.get('source', 'rocprofv3 --pmc')}, same config)"
+
+
+def cpu_info():
+    """nproc, the lscpu model name and the cgroup CPU quota of this host."""
+    import subprocess
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model,
+            "cgroup_cpu_quota": quota}
 
 
 def stereo_cubemap(a, dev, rank, world, backend):
@@ -289,10 +358,14 @@ def stereo_cubemap(a, dev, rank, world, backend):
 
 def cpu_baseline(ses, a):
     """The oracle (CPU restatement of the reference path) on a bounded, centred band of the
-    same frame: a.cpu_rows rows x full width, same spp/depth/scene/camera."""
+    same frame (a.cpu_rows rows x full width, same spp/depth/scene/camera), on every logical
+    core this process may run on (the reference default numThreads=0 -> all cores,
+    common/sys/taskscheduler.cpp:105), one worker thread each over a dynamic
+    16x16 tile queue."""
     import oracle
     blob = ses.export_frame()
-    threads = min(16, oracle.cpu_count())
+    info = cpu_info()
+    threads = info["affinity"]
     y0 = (a.size - a.cpu_rows) // 2
     t = time.perf_counter()
     _, st = oracle.render(blob, a.size, a.size, ses.info()["gamma"], rect=(0, y0, a.size, y0 + a.cpu_rows),
@@ -302,8 +375,8 @@ def cpu_baseline(ses, a):
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"rows [{y0},{y0 + a.cpu_rows}) x {a.size} px at {a.spp} spp of the same frame "
                       f"({rays:.0f} rays in {dt:.1f} s)",
-            "samples_per_s": round(st["samples"] / dt, 1)}
-
+            "samples_per_s": round(st["samples"] / dt, 1), "nproc": info["nproc"], "cpu_model": info["model"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"]}
 
 if __name__ == "__main__":
     main()

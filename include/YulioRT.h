@@ -7,9 +7,12 @@
  *   - one render at a time; StartRT returns after spawning the worker thread;
  *   - WaitRT joins it; StopRT(keepResults) requests a cooperative stop and joins;
  *   - errors are sticky in the status tracker (GetLastErrorRT / GetCurrentStatusRT.lastError).
- * Extension (documented in INTEGRATION.md): besides .dae (Collada — not yet supported by this
- * build, reported as InvalidColladaFormat), StartRT accepts .ecs command files and .xml/.obj
- * scenes, rendered as a stereo cube strip like the reference's non-FPR branch.
+ * Input: a Collada .dae goes through this build's own Collada loader with the Yulio semantics
+ * of devices/device/loaders/ColladaLoader.cpp (FPR cameras YULIO_FPR_VIEW_*, faceCamera meshes
+ * YULIO_CAMERA_ALIGNED_*) and the FPR stereo loop (renderer.cpp:543-737); a file the loader
+ * rejects or one without FPR cameras reports InvalidColladaFormat. Extension:
+ * StartRT also accepts .ecs command files and .xml/.obj scenes, rendered as a stereo cube strip
+ * like the reference's non-FPR branch.
  */
 #ifndef YULIO_RT_H
 #define YULIO_RT_H

@@ -23,6 +23,7 @@ def build():
 
 if not LIB.exists():
     build()
+REF_LIB = HERE / "_ref" / "libref_kat.so"  # reference-compiled KAT library (make -C oracle ref)
 _lib = C.CDLL(str(LIB))
 
 vp, sz, i32, PF = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_float)
@@ -47,6 +48,9 @@ _sig("oracle_sample_table", i32, i32, i32, i32, i32, i32, C.c_char_p, vp, sz)
 _sig("oracle_pixel_sets", None, i32, i32, i32, vp)
 _sig("oracle_scene_triangles", i32, vp, sz, vp, i32)
 _sig("oracle_last_error", C.c_char_p)
+_sig("oracle_random_floats", None, i32, i32, vp)
+_sig("oracle_permutations", None, i32, i32, i32, vp)
+_sig("oracle_shuffles", None, i32, i32, i32, vp)
 
 
 def _err():
@@ -96,6 +100,24 @@ def count_visits(nodes: np.ndarray, tris: np.ndarray, org4, dir4, any_hit=False,
 def random_ints(seed, n):
     out = np.zeros(n, np.int32)
     _lib.oracle_random_ints(seed, n, out.ctypes.data)
+    return out
+
+
+def random_floats(seed, n):
+    out = np.zeros(n, np.float32)
+    _lib.oracle_random_floats(seed, n, out.ctypes.data)
+    return out
+
+
+def permutations(size, seed, count):
+    out = np.zeros((count, size), np.int32)
+    _lib.oracle_permutations(size, seed, count, out.ctypes.data)
+    return out
+
+
+def shuffles(n, seed, count):
+    out = np.zeros((count, n), np.uint32)
+    _lib.oracle_shuffles(n, seed, count, out.ctypes.data)
     return out
 
 

@@ -1018,6 +1018,34 @@ static void perm_make(int* p, int n, Rnd* r) {
     int t = p[i]; p[i] = p[j]; p[j] = t;
   }
 }
+/* KAT exports of the integer layer (pinned against oracle/_ref, tests/test_ref_pin.py) */
+void oracle_permutations(int size, int seed, int count, int32_t* out) {
+  Rnd r;
+  rnd_seed(&r, seed);
+  int* p = (int*)malloc(sizeof(int) * size);
+  for (int c = 0; c < count; ++c) {
+    perm_make(p, size, &r);
+    for (int i = 0; i < size; ++i) out[(size_t)c * size + i] = p[i];
+  }
+  free(p);
+}
+/* vector_t::shuffle (common/sys/stl/vector.h:129-133) of 0..n-1, count times in place */
+void oracle_shuffles(int n, int seed, int count, uint32_t* out) {
+  Rnd r;
+  rnd_seed(&r, seed);
+  uint32_t* v = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  for (int i = 0; i < n; ++i) v[i] = (uint32_t)i;
+  for (int c = 0; c < count; ++c) {
+    for (int k = 0; k < n; k++) { int j = rnd_int(&r) % n; uint32_t t = v[k]; v[k] = v[j]; v[j] = t; }
+    for (int i = 0; i < n; ++i) out[(size_t)c * n + i] = v[i];
+  }
+  free(v);
+}
+void oracle_random_floats(int seed, int n, float* out) {
+  Rnd r;
+  rnd_seed(&r, seed);
+  for (int i = 0; i < n; ++i) out[i] = rnd_float(&r);
+}
 /* jittered (samplers/patterns.h:28-35) */
 static void jittered_(float* s, int n, Rnd* r) {
   const float scale = 1.0f / (float)(uint32_t)n;

@@ -72,6 +72,11 @@ int oracle_count_visits(const void* nodes, size_t numNodes, const void* tris, si
 
 /* Reference Random (common/math/random.h): n draws of getInt() after setSeed(seed). */
 void oracle_random_ints(int seed, int n, int32_t* out);
+/* Random::getFloat (random.h:71), Permutation(size, rng) (permutation.h:42-48) `count` times
+ * from one generator, vector_t::shuffle (vector.h:129-133) `count` times in place. */
+void oracle_random_floats(int seed, int n, float* out);
+void oracle_permutations(int size, int seed, int count, int32_t* out);
+void oracle_shuffles(int n, int seed, int count, uint32_t* out);
 /* SamplerFactory::init sample table: dims as in the GPU table ([dim][set*spp+s]);
  * returns the record count (sets*spp, spp rounded up to a power of two). */
 int oracle_sample_table(int spp, int sets, int iteration, int num1D, int num2D, const char* filter, float* out,

@@ -18,7 +18,7 @@ import yrt  # noqa: E402
 from helpers import c1_args, c2_args, c3_args, c4_args  # noqa: E402
 
 dev = yrt.Device(0)
-threads = min(16, oracle.cpu_count())
+threads = oracle.cpu_count()  # all logical cores
 
 
 def gpu_frames(ses, faces, reps=2):

@@ -1,23 +1,27 @@
 #!/bin/bash
-# GPU-box: PMC counter passes (one rocprofv3 run per counter group, kernel trace only)
-# on a reduced bench frame; summaries go to gpurun_out/pmc_<tag>/.
-mkdir -p gpurun_out
+# GPU-box: PMC counter passes of the bench workload (one rocprofv3 run per counter group,
+# kernel trace only, each under its own time limit) + the VALU calibration kernel, then
+# tools/pmc_json.py -> gpurun_out/pmc_<tag>/pmc.json (copy to profiles/pmc_c3.json).
+# usage: tools/gpu_pmc.sh <tag> ["<bench args>"]
+set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-dev}
-ARGS=${2:-"--size 1024 --spp 16 --steps 1 --warmup 0 --no-cpu-baseline --capture 256"}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$TAG
+ARGS=${2:-""}
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
-           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU" "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
-           "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  cd /tmp && timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
-     python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT/p$i.log 2>&1
+  cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
+     python3 $R/bench.py --steps 1 --warmup 0 --capture 0 --no-cpu-baseline $ARGS > $OUT/p$i.log 2>&1
   rc=$?
   echo "pass $i ($grp) rc=$rc"
-  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; fi
-  [ $rc -ge 124 ] && exit $rc
+  if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
-python3 $GRAFT_REPO_ROOT/tools/pmc_summary.py $OUT > $OUT/summary.txt; cat $OUT/summary.txt
-exit 0
+cd /tmp && timeout -k 10 -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
+   --output-format csv -d $OUT/calib -o run -- $R/tools/valu_calib > $OUT/calib.log 2>&1
+rc=$?; echo "calib rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/calib.log; exit $rc; }
+cd $R && python3 tools/pmc_json.py $OUT $OUT/pmc.json > /dev/null && echo "pmc.json written"

@@ -32,20 +32,12 @@ struct GpuNode {
 };
 static_assert(sizeof(GpuNode) == 128, "node is one 128-B line");
 
-// YRT_TRI_NG: 64-B records that also carry Ng = cross(e1, e2), computed on the host with the
-// device's operation order (IEEE, no contraction), so the test skips the cross product.
-#ifndef YRT_TRI_NG
-#define YRT_TRI_NG 0
-#endif
 struct GpuTri {
   float v0[4];  // xyz, w = global triangle id (bits)
   float e1[4];  // xyz, w = flags (bits): bit0 cullBackFaces
   float e2[4];  // xyz, w unused
-#if YRT_TRI_NG
-  float ng[4];  // cross(e1, e2), w unused
-#endif
 };
-static_assert(sizeof(GpuTri) == (YRT_TRI_NG ? 64 : 48), "tri record size");
+static_assert(sizeof(GpuTri) == 48, "tri record size");
 
 struct GpuGeom {
   int32_t kind, material, light, flags;

@@ -565,6 +565,12 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
   out.maxDepth = C.maxStack;
   if (C.maxStack > stackDepth - 1)
     throw std::runtime_error("BVH traversal stack bound exceeds YRT_STACK_DEPTH");
+  // child references pack (index << 5) | count into an int and the traversal addresses a node
+  // as (index << 7) bytes in 32 bits (kernels/yrt_traverse.h box4_ordered): bound both
+  if (C.out.size() >= (size_t(1) << 25))
+    throw std::runtime_error("BVH exceeds 2^25 nodes (32-bit node byte offsets)");
+  if (leafIds.size() >= (size_t(1) << 26))
+    throw std::runtime_error("BVH exceeds 2^26 leaf triangle references (child reference packing)");
   out.nodes = std::move(C.out);
   const size_t S = leafIds.size();
   out.order = leafIds;
@@ -577,13 +583,6 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
     g.v0[0] = t[0]; g.v0[1] = t[1]; g.v0[2] = t[2];
     g.e1[0] = t[0] - t[3]; g.e1[1] = t[1] - t[4]; g.e1[2] = t[2] - t[5];
     g.e2[0] = t[6] - t[0]; g.e2[1] = t[7] - t[1]; g.e2[2] = t[8] - t[2];
-#if YRT_TRI_NG
-    // cross(e1, e2) in the device's order (common/yrt_math.h)
-    g.ng[0] = g.e1[1] * g.e2[2] - g.e1[2] * g.e2[1];
-    g.ng[1] = g.e1[2] * g.e2[0] - g.e1[0] * g.e2[2];
-    g.ng[2] = g.e1[0] * g.e2[1] - g.e1[1] * g.e2[0];
-    g.ng[3] = 0.f;
-#endif
     int gid = id;
     uint32_t fl = flags[id];
     memcpy(&g.v0[3], &gid, 4);

@@ -299,9 +299,6 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
-#ifndef YRT_NODE_LOOP
-#define YRT_NODE_LOOP 1  // +1.5 % on C3 (node steps chained without the refill block)
-#endif
 #ifndef YRT_TRACE_WAVES
 // 6: a scheduling target — the 16 KB LDS stack of a 128-lane block holds the kernels at 5
 // waves/SIMD, but code scheduled for 6 (78/74 VGPRs with SGPR-based node addressing) runs
@@ -327,28 +324,6 @@ __device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restric
   }
 }
 
-#ifndef YRT_QCURSOR
-#define YRT_QCURSOR 0  // wave-uniform segment cursor, LDS 16384 B per block: measured -0.2 % (noise level), off
-#endif
-#if YRT_QCURSOR && defined(YRT_PREFETCH) && YRT_PREFETCH
-#error "YRT_PREFETCH uses the LDS prefix table: build it with YRT_QCURSOR=0"
-#endif
-#ifndef YRT_PREFETCH
-#define YRT_PREFETCH 0  // prefetched refill: -0.3 % at refill 24, -1.2/-2.5/-3.0 % at 16/8/4: off
-#endif
-#ifndef YRT_POP_CULL
-#define YRT_POP_CULL 0  // measured -2.0 % on C3 (trace closest 352 -> 372 ms/frame): off
-#endif
-// 8-bit lower bound of a non-negative entry distance: float bits >> 20 (exponent + 3 mantissa
-// bits, rounded down) offset to the window [2^-16, 2^16); below it code 0 (no bound), above
-// it clamped to 255 (still a lower bound). Needs node and triangle indices below 2^19.
-#define YRT_TCODE_BASE ((127 - 16) << 3)
-__device__ __forceinline__ int yrt_tag(int c, float t, unsigned codeHi) {
-  const int k = min(max((__float_as_int(t) >> 20) - YRT_TCODE_BASE, 0), 255);
-  return (int)(((unsigned)k << 24) & codeHi) | c;
-}
-__device__ __forceinline__ float yrt_tlower(unsigned k) { return __uint_as_float((k + YRT_TCODE_BASE) << 20); }
-
 template <bool ANY>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
@@ -358,18 +333,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
                                                          ShadowFuse sf) {
   __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
-#if YRT_QCURSOR
-  // Wave-uniform cursor over the queue segments instead of a block-wide prefix table in LDS:
-  // the table's 132 bytes put a block over 16 KB and cost a resident block per CU (9 -> 10
-  // blocks of 128 lanes), and a refill's logical -> physical mapping becomes a compare per
-  // segment its range touches (usually one) instead of a 5-step LDS binary search.
-  unsigned n = 0;
-  for (int k = 0; k < numSegs; ++k) n += counts[(size_t)k * YRT_QCSTRIDE];
-#else
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
   const unsigned n = qm.pre[YRT_QSEGS];
-#endif
   const int lane = lane_id();
   const unsigned wavesPerBlock = YRT_TRACE_BLOCK / 64;
   const unsigned gw = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
@@ -379,16 +345,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   unsigned next = gw * chunk;
   const unsigned end = min(n, next + chunk);
   if (next >= end) return;  // wave-uniform
-#if YRT_QCURSOR
-  // [segLo, segHi): logical range of segment seg, the one holding `next`
-  int seg = 0;
-  unsigned segLo = 0, segHi = counts[0];
-  while (segHi <= next) {
-    seg += 1;
-    segLo = segHi;
-    segHi += counts[(size_t)seg * YRT_QCSTRIDE];
-  }
-#endif
 
   const GpuNode* __restrict__ nodes = sv.nodes;
   const GpuTri* __restrict__ tris = sv.tris;
@@ -412,26 +368,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     stack[YRT_SLOT(sp)] = (e);                                                    \
     sp += 1;                                                                      \
   } while (0)
-  // Closest-hit rays: an entry's top 8 bits hold a lower bound of the child's entry
-  // distance (yrt_tcode); a popped entry the current hit has overtaken is dropped without
-  // fetching it — exactly the entries whose own box test against best.t would fail.
-  const bool popCull = YRT_POP_CULL && !ANY && sv.numNodes < (1 << 19) && sv.numTris < (1 << 19);
-  const unsigned codeHi = popCull ? 0xff000000u : 0u;
 #define YRT_POP()                                                                 \
   do {                                                                            \
-    while (true) {                                                                \
-      if (sp == 0) {                                                              \
-        curCnt = -1;                                                              \
-        break;                                                                    \
-      }                                                                           \
+    if (sp == 0) {                                                                \
+      curCnt = -1;                                                                \
+    } else {                                                                      \
       sp -= 1;                                                                    \
       const unsigned e_ = (unsigned)stack[YRT_SLOT(sp)];                          \
       if (sp >= YRT_LDS_STACK) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - YRT_LDS_STACK) * spillStride]; \
-      const unsigned k_ = (e_ & codeHi) >> 24;                                    \
-      if (k_ != 0u && yrt_tlower(k_) > best.t * YRT_BOX_ROBUST) continue;         \
-      curIdx = (int)((e_ & ~codeHi) >> 5);                                        \
+      curIdx = (int)(e_ >> 5);                                                    \
       curCnt = (int)(e_ & 31u);                                                   \
-      break;                                                                      \
     }                                                                             \
   } while (0)
   // ray kept as plain vectors across iterations (a loop-carried RayPre struct ends up in
@@ -441,20 +387,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   best.t = best.u = best.v = 0.f;
   best.tri = -1;
   const unsigned long long ltMask = (1ull << lane) - 1ull;
-#if YRT_PREFETCH
-  // The next 64 rays of the chunk, [next, next + 64), are loaded ahead: ray i sits in lane
-  // i mod 64. A refill takes its rays from the owning lanes (ds_bpermute) and the lanes whose
-  // rays were taken load the ray 64 further on, so the loads overlap the traversal steps
-  // instead of stalling the refill.
-  unsigned pfLi = next + ((unsigned)(lane - (int)next) & 63u);
-  int pfQ = 0;
-  float4 pfO = make_float4(0.f, 0.f, 0.f, 0.f), pfD = pfO;
-  if (pfLi < end) {
-    pfQ = qmap_phys(qm, segCap, pfLi);
-    pfO = org[pfQ];
-    pfD = dir[pfQ];
-  }
-#endif
 
 #ifdef YRT_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -472,52 +404,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     YRT_PROF(1, 64 - nIdle);
     if (nIdle >= YRT_REFILL) {
       if (next < end) {
-#if YRT_PREFETCH
-        const unsigned li = next + (unsigned)__popcll(idle & ltMask);
-        const int src = (int)(li & 63u);
-        const int q2 = __shfl(pfQ, src, 64);
-        const float4 o2 = make_float4(__shfl(pfO.x, src, 64), __shfl(pfO.y, src, 64), __shfl(pfO.z, src, 64),
-                                      __shfl(pfO.w, src, 64));
-        const float4 d2 = make_float4(__shfl(pfD.x, src, 64), __shfl(pfD.y, src, 64), __shfl(pfD.z, src, 64),
-                                      __shfl(pfD.w, src, 64));
-        if (pfLi < next + (unsigned)nIdle) {
-          pfLi += 64u;
-          if (pfLi < end) {
-            pfQ = qmap_phys(qm, segCap, pfLi);
-            pfO = org[pfQ];
-            pfD = dir[pfQ];
-          }
-        }
-        if (!has) {
-          if (li < end) {
-            q = q2;
-            ro = o2;
-            rd = d2;
-#elif YRT_QCURSOR
-        const unsigned li = next + (unsigned)__popcll(idle & ltMask);
-        {
-          // segments covering [next, min(next + nIdle, end)), walked wave-uniformly
-          const unsigned hiLi = min(next + (unsigned)nIdle, end);
-          while (true) {
-            if (!has && li >= segLo && li < segHi) q = seg * segCap + (int)(li - segLo);
-            if (segHi >= hiLi) break;
-            seg += 1;
-            segLo = segHi;
-            segHi += counts[(size_t)seg * YRT_QCSTRIDE];
-          }
-        }
-        if (!has) {
-          if (li < end) {
-            ro = org[q];
-            rd = dir[q];
-#else
         if (!has) {
           const unsigned li = next + (unsigned)__popcll(idle & ltMask);
           if (li < end) {
             q = qmap_phys(qm, segCap, li);
             ro = org[q];
             rd = dir[q];
-#endif
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
             best.t = rd.w;
@@ -561,51 +453,34 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     const int nNode = __popcll(__ballot(has && curCnt == 0));
     const int nBlocked = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
     if (nNode * 4 > nBlocked * YRT_NODE_BIAS) {
-#if YRT_NODE_LOOP
-     // consecutive node steps without the retire/refill block in between
+     // consecutive node steps without the retire/refill block in between (+1.5 % on C3)
      while (true) {
-#endif
       YRT_PROF(2, 1);
       YRT_PROF(3, __popcll(__ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
         float t[4];
         int c[4];
-#ifndef YRT_ORDERED_PLANES
-// 1 (default): sign-ordered planes in both kernels, at 5 waves/SIMD (+1.5% on C3 with two
-// lanes); at 6 waves the closest-hit kernel's six per-lane plane addresses pushed it to the
-// 80-VGPR cap and it ran 11% slower. 2 = shadow rays only, 0 = neither
-#define YRT_ORDERED_PLANES 1
-#endif
-        if (YRT_ORDERED_PLANES == 1 || (YRT_ORDERED_PLANES == 2 && ANY))
-          box4_ordered(nodes + curIdx, r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
-        else
-          box4(nodes + curIdx, r, best.t, t, c);
-#ifndef YRT_CHILD_ORDER
-// Child order: 3 (default) = closest-hit rays sort the hit children by entry distance, shadow
-// (any-hit) rays take them in the builder's slot order — front-to-back order buys an any-hit
-// ray nothing, and skipping the 5-comparator network cut k_trace<true> by 9% (profiles/r01).
-// 0 = sort both, 1 = nearest-first only / none for any-hit, 2 = nearest-first for both.
-#define YRT_CHILD_ORDER 3
-#endif
-        if (YRT_CHILD_ORDER == 0 || (YRT_CHILD_ORDER == 3 && !ANY)) sort4(t, c);
-        else if (YRT_CHILD_ORDER == 2 || (YRT_CHILD_ORDER == 1 && !ANY)) nearest4(t, c);
+        // sign-ordered slab planes (+1.5 % on C3 with two lanes, bit-identical distances)
+        box4_ordered(r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
+        // closest-hit rays sort the hit children by entry distance; shadow (any-hit) rays
+        // take them in the builder's slot order — front-to-back order buys an any-hit ray
+        // nothing, and skipping the 5-comparator network cut k_trace<true> by 9 % (profiles/r01)
+        if (!ANY) sort4(t, c);
         // nearest hit child next; the other hits pushed farthest-first
         const float INF = __int_as_float(0x7f800000);
-#ifndef YRT_FAST_PUSH
-#define YRT_FAST_PUSH 1  // shadow rays -4..9%, closest neutral (profiles/r01)
-#endif
-        if (YRT_FAST_PUSH && sp + 3 <= YRT_LDS_STACK) {
+        if (sp + 3 <= YRT_LDS_STACK) {
           // all three candidates fit in free ring slots: store unconditionally, advance sp
-          // only past the hit ones (a store of a missed child lands on a free slot)
+          // only past the hit ones (a store of a missed child lands on a free slot);
+          // shadow rays -4..9 %, closest neutral (profiles/r01)
           const int h3 = t[3] < INF, h2 = t[2] < INF, h1 = t[1] < INF;
-          stack[YRT_SLOT(sp)] = yrt_tag(c[3], t[3], codeHi);
-          stack[YRT_SLOT(sp + h3)] = yrt_tag(c[2], t[2], codeHi);
-          stack[YRT_SLOT(sp + h3 + h2)] = yrt_tag(c[1], t[1], codeHi);
+          stack[YRT_SLOT(sp)] = c[3];
+          stack[YRT_SLOT(sp + h3)] = c[2];
+          stack[YRT_SLOT(sp + h3 + h2)] = c[1];
           sp += h3 + h2 + h1;
         } else {
-          if (t[3] < INF) YRT_PUSH(yrt_tag(c[3], t[3], codeHi));
-          if (t[2] < INF) YRT_PUSH(yrt_tag(c[2], t[2], codeHi));
-          if (t[1] < INF) YRT_PUSH(yrt_tag(c[1], t[1], codeHi));
+          if (t[3] < INF) YRT_PUSH(c[3]);
+          if (t[2] < INF) YRT_PUSH(c[2]);
+          if (t[1] < INF) YRT_PUSH(c[1]);
         }
         if (t[0] < INF) {
           curIdx = c[0] >> 5;
@@ -619,12 +494,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
       }
-#if YRT_NODE_LOOP
       const int nNode2 = __popcll(__ballot(has && curCnt == 0));
       const int nBlocked2 = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
       if (!(nNode2 * 4 > nBlocked2 * YRT_NODE_BIAS)) break;
      }
-#endif
     } else {
       // leaf step: the parked leaf, or else the current entry when it is a leaf
       const bool usePend = pendCnt > 0;
@@ -1535,11 +1408,6 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ t
     t.v0[0] = a.x; t.v0[1] = a.y; t.v0[2] = a.z;
     t.e1[0] = a.x - b.x; t.e1[1] = a.y - b.y; t.e1[2] = a.z - b.z;
     t.e2[0] = c.x - a.x; t.e2[1] = c.y - a.y; t.e2[2] = c.z - a.z;
-#if YRT_TRI_NG
-    t.ng[0] = t.e1[1] * t.e2[2] - t.e1[2] * t.e2[1];
-    t.ng[1] = t.e1[2] * t.e2[0] - t.e1[0] * t.e2[2];
-    t.ng[2] = t.e1[0] * t.e2[1] - t.e1[1] * t.e2[0];
-#endif
   }
 }
 

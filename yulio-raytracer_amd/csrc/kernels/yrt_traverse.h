@@ -96,23 +96,14 @@ __device__ __forceinline__ int plane_offsets(float ix, float iy, float iz) {
   return ((__float_as_uint(ix) >> 27) & 16) | ((__float_as_uint(iy) >> 19) & (16 << 8)) |
          ((__float_as_uint(iz) >> 11) & (16 << 16));
 }
-// YRT_EMPTY_INF: empty slots carry inverted infinite boxes (device/bvh_build.cpp), which the
-// ordered-plane test culls by itself — the child-reference check is skipped.
-#ifndef YRT_EMPTY_INF
-#define YRT_EMPTY_INF 1
-#endif
-// YRT_NODE_SADDR: the six plane loads and the child load address the node array as a uniform
-// (SGPR) base plus a 32-bit per-lane byte offset (global_load saddr form) instead of six
-// 64-bit per-lane pointers.
-#ifndef YRT_NODE_SADDR
-#define YRT_NODE_SADDR 1
-#endif
-__device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, const RayPre& r, int planeOff,
-                                             float tmax, float t[4], int c[4], const GpuNode* __restrict__ base,
-                                             int nodeIdx) {
+// Empty slots carry inverted infinite boxes (device/bvh_build.cpp), which the ordered-plane
+// test culls by itself, so no child-reference check is needed. The six plane loads and the
+// child load address the node array as a uniform (SGPR) base plus a 32-bit per-lane byte
+// offset (global_load saddr form) instead of six 64-bit per-lane pointers (78/74 VGPRs instead
+// of 82/84). nodeIdx < 2^25 (node byte offsets fit 32 bits; bvh_build.cpp enforces it).
+__device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
+                                             const GpuNode* __restrict__ base, int nodeIdx) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-#if YRT_NODE_SADDR
-  (void)np;
   const char* b0 = (const char*)base;
   const unsigned nb = (unsigned)nodeIdx << 7;
   const unsigned ox = (unsigned)planeOff & 0xffu, oy = ((unsigned)planeOff >> 8) & 0xffu,
@@ -121,16 +112,6 @@ __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, con
   const float4 ny = *(const float4*)(b0 + (nb + (32u + oy))), fy = *(const float4*)(b0 + (nb + (48u - oy)));
   const float4 nz = *(const float4*)(b0 + (nb + (64u + oz))), fz = *(const float4*)(b0 + (nb + (80u - oz)));
   const int4 ch = *(const int4*)(b0 + (nb + 96u));
-#else
-  (void)base;
-  (void)nodeIdx;
-  const char* b = (const char*)np;
-  const int ox = planeOff & 0xff, oy = (planeOff >> 8) & 0xff, oz = planeOff >> 16;
-  const float4 nx = *(const float4*)(b + ox), fx = *(const float4*)(b + (16 - ox));
-  const float4 ny = *(const float4*)(b + 32 + oy), fy = *(const float4*)(b + (48 - oy));
-  const float4 nz = *(const float4*)(b + 64 + oz), fz = *(const float4*)(b + (80 - oz));
-  const int4 ch = *(const int4*)(b + 96);
-#endif
   const f2 ox2 = {r.org.x, r.org.x}, oy2 = {r.org.y, r.org.y}, oz2 = {r.org.z, r.org.z};
   const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
   const f2 nx01 = (f2{nx.x, nx.y} - ox2) * ix, nx23 = (f2{nx.z, nx.w} - ox2) * ix;
@@ -144,7 +125,7 @@ __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, con
   do {                                                                           \
     const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                   \
     const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                      \
-    t[k] = (nn <= ff * YRT_BOX_ROBUST && (YRT_EMPTY_INF || (CH) != -1)) ? nn : INF; \
+    t[k] = nn <= ff * YRT_BOX_ROBUST ? nn : INF;                                 \
     c[k] = (CH);                                                                 \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
@@ -152,23 +133,6 @@ __device__ __forceinline__ void box4_ordered(const GpuNode* __restrict__ np, con
   YRT_CHILD(2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x, ch.z);
   YRT_CHILD(3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y, ch.w);
 #undef YRT_CHILD
-}
-
-// Moves the nearest (t, child) pair to slot 0 (3 comparators); the others keep no order.
-__device__ __forceinline__ void nearest4(float t[4], int c[4]) {
-#define YRT_CSWAP(a, b)                          \
-  do {                                           \
-    const bool sw = t[b] < t[a];                 \
-    const float ta = sw ? t[b] : t[a];           \
-    const float tb = sw ? t[a] : t[b];           \
-    const int ca = sw ? c[b] : c[a];             \
-    const int cb = sw ? c[a] : c[b];             \
-    t[a] = ta; t[b] = tb; c[a] = ca; c[b] = cb;  \
-  } while (0)
-  YRT_CSWAP(0, 1);
-  YRT_CSWAP(2, 3);
-  YRT_CSWAP(0, 2);
-#undef YRT_CSWAP
 }
 
 // Sorts the four (t, child) pairs by t ascending (5-comparator network, stable for equal t).
@@ -197,11 +161,7 @@ __device__ __forceinline__ bool tri_test_t(const GpuTri& tr, const RayPre& r, fl
   V3 v0 = v3(tr.v0[0], tr.v0[1], tr.v0[2]);
   V3 e1 = v3(tr.e1[0], tr.e1[1], tr.e1[2]);
   V3 e2 = v3(tr.e2[0], tr.e2[1], tr.e2[2]);
-#if YRT_TRI_NG
-  V3 Ng = v3(tr.ng[0], tr.ng[1], tr.ng[2]);
-#else
   V3 Ng = cross(e1, e2);
-#endif
   V3 C = v0 - r.org;
   V3 R = cross(r.dir, C);
   float den = dot(Ng, r.dir);
