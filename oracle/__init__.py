@@ -60,6 +60,7 @@ def _err():
 
 def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0):
     """RGB_FLOAT32 image (H, W, 3) of the frame blob; pixels outside rect stay NaN."""
+    threads = threads or cpu_count()
     x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
     out = np.full((height, width, 3), np.nan, np.float32)
     st = OracleStats()
@@ -147,4 +148,13 @@ def scene_triangles(blob: bytes):
 
 
 def cpu_count():
-    return len(os.sched_getaffinity(0))
+    """CPUs this process can use: the affinity mask, capped at the cgroup CPU quota (the GPU
+    box grants a 16-CPU share of a larger host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            n = max(1, min(n, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n

@@ -115,6 +115,8 @@ def test_intersect_golden_records(gpu_device, name):
 
 
 # ----------------------------------------------------------------------------- full renders
+# Every render comparison uses the SURVEY §8(d) gate at its stated bound: |g-c| <= 1e-3 +
+# 1e-3|c| on >= 99.9 % (C1/C2) / 99.5 % (C3-C5) of channels and mean-abs-diff <= 1e-4 * mean.
 def test_c1_pathtracer_parity(gpu_device):
     img, ref, st = _render_pair(gpu_device, c1_args(256, 1))
     parity(img, ref, 0.999)
@@ -126,29 +128,114 @@ def test_c2_pathtracer_parity(gpu_device):
     parity(img, ref, 0.999)
 
 
+def test_c2_full_size_parity(gpu_device):
+    """C2 at its BASELINE size: cornell_box_spheres 1024^2 at 16 spp, the whole frame."""
+    img, ref, st = _render_pair(gpu_device, c2_args(1024, 16))
+    r = parity(img, ref, 0.999)
+    assert st["samples"] == 1024 * 1024 * 16
+    print("C2 1024^2 16spp", r)
+
+
 def test_c3_standin_parity(gpu_device):
     img, ref, _ = _render_pair(gpu_device, c3_args(128, 4))
-    parity(img, ref, 0.995, mad_rel=1e-3)
+    parity(img, ref, 0.995)
 
 
 def test_c3_full_size_band_parity(gpu_device):
     """C3 at its BASELINE size (2048^2, 64 spp, depth 10, 64 M-path batches over two lanes):
-    the GPU frame against the oracle on a centred band of 8 full rows (same frame blob)."""
+    the GPU frame against the oracle on a centred band of 64 full rows (same frame blob)."""
     s = _session(gpu_device, c3_args(2048, 64))
     info = s.info()
     img = s.render()
-    y0 = 1020
-    ref, _ = oracle.render(s.export_frame(), 2048, 2048, info["gamma"], rect=(0, y0, 2048, y0 + 8),
-                           threads=min(16, oracle.cpu_count()))
-    parity(img[y0:y0 + 8], ref[y0:y0 + 8], 0.995, mad_rel=1e-3)
+    y0 = 992
+    ref, _ = oracle.render(s.export_frame(), 2048, 2048, info["gamma"], rect=(0, y0, 2048, y0 + 64))
+    r = parity(img[y0:y0 + 64], ref[y0:y0 + 64], 0.995)
     assert np.isfinite(img).all()
+    print("C3 band", r)
     s.close()
 
 
 @pytest.mark.parametrize("face", [0, 3, 7, 10])
 def test_c4_stereo_face_parity(gpu_device, face):
     img, ref, _ = _render_pair(gpu_device, c4_args(96, 4), face=face)
-    parity(img, ref, 0.995, mad_rel=1e-3)
+    parity(img, ref, 0.995)
+
+
+def _hdri_scene(L=(2.0, 1.5, 1.2)):
+    """models/test_stereo.xml with the HDRI radiance its authors left commented out
+    (test_stereo.xml:100 `<L>2.0 1.5 1.2</L>`) switched on; texture paths made absolute."""
+    from helpers import SCENES
+    src = (SCENES / "test_stereo.xml").read_text()
+    assert "<L>0.0 0.0 0.0</L>" in src
+    txt = src.replace("<L>0.0 0.0 0.0</L>", "<L>%g %g %g</L>" % L)
+    for f in ("logo.png", "lines.ppm"):
+        txt = txt.replace(f'"{f}"', f'"{SCENES / f}"')
+    out = SCENES / "_generated" / "test_stereo_hdri.xml"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    out.write_text(txt)
+    return out
+
+
+@pytest.mark.parametrize("face", [0, 4, 9])
+def test_hdri_light_parity(gpu_device, face):
+    """HDRILight with non-zero radiance (lights/hdrilight.cpp:39-112): lat-long Le on misses and
+    importance-sampled direct light from the precomputed per-record light samples."""
+    from helpers import SCENES
+    args = ["-i", str(_hdri_scene()), "-c", str(SCENES / "test_stereo_view.ecs"), "-size", "96", "96",
+            "-spp", "4", "-stereo"]
+    img, ref, st = _render_pair(gpu_device, args, face=face)
+    parity(img, ref, 0.995)
+    # the HDRI really contributes: the same face without it is darker
+    img0, _, _ = _render_pair(gpu_device, c4_args(96, 4), face=face)
+    assert img.mean() > img0.mean() * 1.2, (img.mean(), img0.mean())
+
+
+def test_white_furnace_gpu(gpu_device):
+    """KAT 5 on the device: an open Lambertian plane (albedo 0.5) under a constant dome L = 2 with
+    nothing above it: camera rays hitting the plane return L * albedo (one diffuse vertex, the
+    dome sample's Lambertian weight is exactly albedo), sky pixels L, and the image equals the
+    oracle's."""
+    from test_cpu_host import yrt_lookat
+    d = gpu_device
+    L, albedo = 2.0, 0.5
+    mesh = d.rtNewShape("trianglemesh")
+    pos = np.array([[-1e3, 0, -1e3], [1e3, 0, -1e3], [1e3, 0, 1e3], [-1e3, 0, 1e3]], np.float32)
+    idx = np.array([[0, 2, 1], [0, 3, 2]], np.int32)
+    dp, di = d.rtNewData("immutable", pos), d.rtNewData("immutable", idx)
+    d.rtSetArray(mesh, "positions", "float3", dp, 4, 12)
+    d.rtSetArray(mesh, "indices", "int3", di, 2, 12)
+    d.rtCommit(mesh)
+    mat = d.rtNewMaterial("Matte")
+    d.rtSetFloat3(mat, "reflectance", albedo, albedo, albedo)
+    d.rtCommit(mat)
+    amb = d.rtNewLight("ambientlight")
+    d.rtSetFloat3(amb, "L", L, L, L)
+    d.rtCommit(amb)
+    scene = d.rtNewScene("default")
+    d.rtSetPrimitive(scene, 0, d.rtNewShapePrimitive(mesh, mat))
+    d.rtSetPrimitive(scene, 1, d.rtNewLightPrimitive(amb))
+    d.rtCommit(scene)
+    cam = d.rtNewCamera("pinhole")
+    d.rtSetTransform(cam, "local2world", yrt_lookat((0, 10, 0), (0, 10, 1), (0, 1, 0)))
+    d.rtSetFloat1(cam, "angle", 60.0)
+    d.rtSetFloat1(cam, "aspectRatio", 1.0)
+    d.rtCommit(cam)
+    r = d.rtNewRenderer("pathtracer")
+    d.rtSetInt1(r, "maxDepth", 2)
+    d.rtSetInt1(r, "sampler.spp", 4)
+    d.rtSetFloat1(r, "tMaxShadowRay", 1e4)
+    d.rtCommit(r)
+    tm = d.rtNewToneMapper("default")
+    d.rtCommit(tm)
+    fb = d.rtNewFrameBuffer("RGB_FLOAT32", 64, 64)
+    d.rtRenderFrame(r, cam, scene, tm, fb, 0)
+    img = d.framebuffer_array(fb, 64, 64, "RGB_FLOAT32")
+    ref, _ = oracle.render(d.export_frame(r, cam, scene), 64, 64, 1.0)
+    parity(img, ref, 0.999)
+    plane = np.isclose(img, L * albedo, rtol=2e-3)
+    sky = np.isclose(img, L, rtol=2e-3)
+    assert plane.mean() > 0.3 and sky.mean() > 0.3, (plane.mean(), sky.mean())
+    assert (img >= L * albedo * (1 - 2e-3)).all() and (img <= L * (1 + 2e-3)).all()
 
 
 # ----------------------------------------------------------------------------- invariances
