@@ -51,6 +51,7 @@ _sig("oracle_last_error", C.c_char_p)
 _sig("oracle_random_floats", None, i32, i32, vp)
 _sig("oracle_permutations", None, i32, i32, i32, vp)
 _sig("oracle_shuffles", None, i32, i32, i32, vp)
+_sig("oracle_libm", None, i32, i32, vp, vp, vp)
 
 
 def _err():
@@ -107,6 +108,18 @@ def random_ints(seed, n):
 def random_floats(seed, n):
     out = np.zeros(n, np.float32)
     _lib.oracle_random_floats(seed, n, out.ctypes.data)
+    return out
+
+
+LIBM = {"sin": 0, "cos": 1, "exp": 2, "log": 3, "pow": 4, "asin": 5, "acos": 6, "atan": 7, "atan2": 8}
+
+
+def libm(fn, x, y=None):
+    """yrt_libm.h (the per-ray path's elementary functions, shared with the device) on float32 x[, y]."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), np.float32)
+    out = np.zeros_like(x)
+    _lib.oracle_libm(LIBM[fn], x.size, x.ctypes.data, y.ctypes.data, out.ctypes.data)
     return out
 
 

@@ -3,6 +3,9 @@
 #define _GNU_SOURCE
 #include "yrt_oracle.h"
 
+/* the per-ray path's elementary functions, evaluated exactly as the device does */
+#include "../yulio-raytracer_amd/csrc/common/yrt_libm.h"
+
 #include <math.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -73,7 +76,7 @@ static inline L3 linv(L3 a) {
 }
 static inline L3 lrotate(V3 u_, float r) {
   V3 u = normalize(u_);
-  float s = sinf(r), c = cosf(r);
+  float s = yrt_sinf(r), c = yrt_cosf(r);
   return l3_rows(u.x * u.x + (1 - u.x * u.x) * c, u.x * u.y * (1 - c) - u.z * s, u.x * u.z * (1 - c) + u.y * s,
                  u.x * u.y * (1 - c) + u.z * s, u.y * u.y + (1 - u.y * u.y) * c, u.y * u.z * (1 - c) - u.x * s,
                  u.x * u.z * (1 - c) - u.y * s, u.y * u.z * (1 - c) + u.x * s, u.z * u.z + (1 - u.z * u.z) * c);
@@ -1041,6 +1044,22 @@ void oracle_shuffles(int n, int seed, int count, uint32_t* out) {
   }
   free(v);
 }
+/* the shared elementary functions (yrt_libm.h), for their accuracy tests */
+void oracle_libm(int fn, int n, const float* x, const float* y, float* out) {
+  for (int i = 0; i < n; ++i) {
+    switch (fn) {
+      case 0: out[i] = yrt_sinf(x[i]); break;
+      case 1: out[i] = yrt_cosf(x[i]); break;
+      case 2: out[i] = yrt_expf(x[i]); break;
+      case 3: out[i] = yrt_logf(x[i]); break;
+      case 4: out[i] = yrt_powf(x[i], y[i]); break;
+      case 5: out[i] = yrt_asinf(x[i]); break;
+      case 6: out[i] = yrt_acosf(x[i]); break;
+      case 7: out[i] = yrt_atanf(x[i]); break;
+      default: out[i] = yrt_atan2f(x[i], y[i]); break;
+    }
+  }
+}
 void oracle_random_floats(int seed, int n, float* out) {
   Rnd r;
   rnd_seed(&r, seed);
@@ -1295,7 +1314,7 @@ static void camera_ray(const Camera* C, float fx, float fy, float lx, float ly, 
   if (C->dof) { /* depthoffieldcamera.h:20-26, uniformSampleDisk (shapesampler.h:187-191) */
     const A3 m = C->p2w[0];
     const float r = sqrtf(lx), th = TWO_PI_F * ly;
-    const V3 begin = xfmPoint(C->p2w[1], v3(C->lensRadius * r * cosf(th), C->lensRadius * r * sinf(th), 0.0f));
+    const V3 begin = xfmPoint(C->p2w[1], v3(C->lensRadius * r * yrt_cosf(th), C->lensRadius * r * yrt_sinf(th), 0.0f));
     const V3 end = add(m.p, muls(add(add(muls(m.l.vx, fx), muls(m.l.vy, 1.0f - fy)), m.l.vz), C->focal));
     *org = begin;
     *dir = normalize(sub(end, begin));
@@ -1315,16 +1334,16 @@ static void camera_ray(const Camera* C, float fx, float fy, float lx, float ly, 
   float theta = 0.f, absVA = 0.f;
   if (ef <= 3) {
     const V3 xDir = normalize(add(add(muls(P0.l.vx, fx), muls(P0.l.vy, .5f)), P0.l.vz));
-    theta = acosf(clampf_(dot(xDir, C->xyz), -1.f, 1.f)) * signf_(fx - .5f);
+    theta = yrt_acosf(clampf_(dot(xDir, C->xyz), -1.f, 1.f)) * signf_(fx - .5f);
     const V3 yDir = normalize(add(add(muls(P0.l.vx, .5f), muls(P0.l.vy, yPixel)), P0.l.vz));
-    const float yAngle = rad2deg(acosf(clampf_(dot(yDir, C->xyz), -1.f, 1.f))) * signf_(yPixel - .5f);
+    const float yAngle = rad2deg(yrt_acosf(clampf_(dot(yDir, C->xyz), -1.f, 1.f))) * signf_(yPixel - .5f);
     absVA = fabsf(yAngle);
   } else {
     const V3 xyDirNorm = normalize(v3(fx - .5f, yPixel - .5f, 0.f));
     const V3 xyUp = v3(0.f, ef == 4 ? -1.f : 1.f, 0.f);
-    theta = acosf(clampf_(dot(xyDirNorm, xyUp), -1.f, 1.f)) * signf_(fx - .5f);
+    theta = yrt_acosf(clampf_(dot(xyDirNorm, xyUp), -1.f, 1.f)) * signf_(fx - .5f);
     const V3 xyzDir = normalize(add(add(muls(P0.l.vx, fx), muls(P0.l.vy, yPixel)), P0.l.vz));
-    const float xyzAngle = rad2deg(acosf(clampf_(dot(xyzDir, C->xyz), -1.f, 1.f)));
+    const float xyzAngle = rad2deg(yrt_acosf(clampf_(dot(xyzDir, C->xyz), -1.f, 1.f)));
     absVA = 90.f - fabsf(xyzAngle);
   }
   float eyeOffset = C->eyeSep * (C->face < 6 ? -.5f : .5f);
@@ -1336,7 +1355,7 @@ static void camera_ray(const Camera* C, float fx, float fy, float lx, float ly, 
   const A3 rot = a3_rotate_about(C->origin, C->up, theta);
   const V3 rayOrigin = aamul(rot, p2w).p;
   if (C->toeIn) {
-    const float toe = -atanf(eyeOffset * C->rcpZpd);
+    const float toe = -yrt_atanf(eyeOffset * C->rcpZpd);
     p2w = aamul(a3_rotate_about(rayOrigin, C->up, toe), p2w);
   }
   *org = rayOrigin;
@@ -1452,7 +1471,7 @@ static V3 cos_hemi(float u, float v, V3 N, float* pdf) {
   const float phi = TWO_PI_F * u;
   const float cosT = sqrtf(v), sinT = sqrtf(1.0f - v);
   *pdf = cosT * ONE_OVER_PI_F;
-  return lmul(frame_(N), v3(cosf(phi) * sinT, sinf(phi) * sinT, cosT));
+  return lmul(frame_(N), v3(yrt_cosf(phi) * sinT, yrt_sinf(phi) * sinT, cosT));
 }
 
 static V3 lambert_eval(V3 R, const DG* dg, V3 wi) { return muls(muls(R, ONE_OVER_PI_F), clamp01(dot(wi, dg->Ns))); }
@@ -1475,7 +1494,7 @@ static float aniso_D(float nx, float ny, const DG* dg, V3 wh) {
   const float R = cP * cP + sP * sP;
   if (R == 0.0f) return norm2;
   const float n = (nx * (cP * cP) + ny * (sP * sP)) * rcp(R);
-  return norm2 * powf(fabsf(cT), n);
+  return norm2 * yrt_powf(fabsf(cT), n);
 }
 /* Microfacet<Fresnel,Distribution>::eval (brdfs/microfacet.h:28-41): dielectric or conductor
  * Fresnel, power-cosine or anisotropic power-cosine distribution */
@@ -1492,7 +1511,7 @@ static V3 micro_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
     D = aniso_D(c->a, c->b, dg, wh);
   } else {
     const float n = c->kind == B_MICRO ? c->c : c->a;
-    D = ((n + 2) * ONE_OVER_TWO_PI_F) * powf(fabsf(dot(wh, dg->Ns)), n);
+    D = ((n + 2) * ONE_OVER_TWO_PI_F) * yrt_powf(fabsf(dot(wh, dg->Ns)), n);
   }
   const float G = fminf(fminf(1.0f, 2.0f * cH * cO * rcp(cT)), 2.0f * cH * cI * rcp(cT));
   return muls(mulv(muls(muls(c->R, D), G), F), rcp(4.0f * cO));
@@ -1501,13 +1520,13 @@ static V3 micro_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
 static V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 static V3 minnaert_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const float cI = clamp01(dot(wi, dg->Ns));
-  const float bs = powf(clamp01(dot(wo, wi)), c->a);
+  const float bs = yrt_powf(clamp01(dot(wo, wi)), c->a);
   return divs(muls(muls(c->R, bs), cI), PI_F);
 }
 static V3 velvety_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const float cO = clamp01(dot(wo, dg->Ns)), cI = clamp01(dot(wi, dg->Ns));
   const float sO = sqrtf(1.0f - cO * cO);
-  const float hs = powf(sO, c->a);
+  const float hs = yrt_powf(sO, c->a);
   return divs(muls(muls(c->R, hs), cI), PI_F);
 }
 /* DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38) */
@@ -1527,7 +1546,7 @@ static V3 layer_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
 static V3 spec_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   V3 r = reflect2(wo, dg->Ns);
   if (dot(r, wi) < 0) return vs(0.f);
-  return muls(muls(muls(muls(c->R, c->a + 2), 1.0f / (2.0f * PI_F)), powf(dot(r, wi), c->a)), clamp01(dot(wi, dg->Ns)));
+  return muls(muls(muls(muls(c->R, c->a + 2), 1.0f / (2.0f * PI_F)), yrt_powf(dot(r, wi), c->a)), clamp01(dot(wi, dg->Ns)));
 }
 static V3 brdf_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   switch (c->kind) {
@@ -1568,7 +1587,7 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       const float alpha = c->b * rcp(ct);
       float cT;
       const V3 la = muls(c->R, alpha);
-      return muls(v3(expf(la.x), expf(la.y), expf(la.z)), 1.f - fres2(ct, c->a, &cT));
+      return muls(v3(yrt_expf(la.x), yrt_expf(la.y), yrt_expf(la.z)), 1.f - fres2(ct, c->a, &cT));
     }
     case B_LAYER: { /* dielectriclayer.h:40-62 */
       float cO = dot(wo, dg->Ns);
@@ -1596,11 +1615,11 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       const float n = c->c;
       const float norm1 = (n + 1) * ONE_OVER_TWO_PI_F;
       const float phi = TWO_PI_F * sx;
-      const float cP = cosf(phi), sP = sinf(phi);
-      const float cT = powf(sy, rcp(n + 1));
+      const float cP = yrt_cosf(phi), sP = yrt_sinf(phi);
+      const float cT = yrt_powf(sy, rcp(n + 1));
       const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
       const V3 wh = lmul(frame_(dg->Ns), v3(cP * sT, sP * sT, cT));
-      const float whpdf = norm1 * powf(cT, n);
+      const float whpdf = norm1 * yrt_powf(cT, n);
       *wi = reflect2(wo, wh);
       *pdf = whpdf * rcp(4.0f * fabsf(dot(wo, wh)));
       if (dot(*wi, dg->Ns) <= 0.0f) return vs(0.f);
@@ -1615,11 +1634,11 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       const float n = c->a;
       const float norm1 = (n + 1) * ONE_OVER_TWO_PI_F;
       const float phi = TWO_PI_F * sx;
-      const float cP = cosf(phi), sP = sinf(phi);
-      const float cT = powf(sy, rcp(n + 1));
+      const float cP = yrt_cosf(phi), sP = yrt_sinf(phi);
+      const float cT = yrt_powf(sy, rcp(n + 1));
       const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
       const V3 wh = lmul(frame_(dg->Ns), v3(cP * sT, sP * sT, cT));
-      const float whpdf = norm1 * powf(cT, n);
+      const float whpdf = norm1 * yrt_powf(cT, n);
       *wi = reflect2(wo, wh);
       *pdf = whpdf * rcp(4.0f * fabsf(dot(wo, wh)));
       if (dot(*wi, dg->Ns) <= 0.0f) return vs(0.f);
@@ -1630,14 +1649,14 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       const float nx = c->a, ny = c->b;
       const float norm1 = sqrtf((nx + 1) * (ny + 1)) * ONE_OVER_TWO_PI_F;
       const float phi = TWO_PI_F * sx;
-      const float sP0 = sqrtf(nx + 1) * sinf(phi);
-      const float cP0 = sqrtf(ny + 1) * cosf(phi);
+      const float sP0 = sqrtf(nx + 1) * yrt_sinf(phi);
+      const float cP0 = sqrtf(ny + 1) * yrt_cosf(phi);
       const float nrm = rsqrt_(sP0 * sP0 + cP0 * cP0);
       const float sP = sP0 * nrm, cP = cP0 * nrm;
       const float n = nx * (cP * cP) + ny * (sP * sP);
-      const float cT = powf(sy, rcp(n + 1));
+      const float cT = yrt_powf(sy, rcp(n + 1));
       const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
-      const float whpdf = norm1 * powf(cT, n);
+      const float whpdf = norm1 * yrt_powf(cT, n);
       const V3 h = v3(cP * sT, sP * sT, cT);
       const V3 wh = add(add(muls(dg->Tx, h.x), muls(dg->Ty, h.y)), muls(dg->Ns, h.z));
       *wi = reflect2(wo, wh);
@@ -1668,10 +1687,10 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
     case B_SPEC: { /* specular.h:26-28, shapesampler.h:104-121 */
       const float e = c->a;
       const float phi = TWO_PI_F * sx;
-      const float cT = powf(sy, rcp(e + 1));
+      const float cT = yrt_powf(sy, rcp(e + 1));
       const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
-      *pdf = (e + 1.0f) * powf(cT, e) * ONE_OVER_TWO_PI_F;
-      *wi = lmul(frame_(reflect2(wo, dg->Ns)), v3(cosf(phi) * sT, sinf(phi) * sT, cT));
+      *pdf = (e + 1.0f) * yrt_powf(cT, e) * ONE_OVER_TWO_PI_F;
+      *wi = lmul(frame_(reflect2(wo, dg->Ns)), v3(yrt_cosf(phi) * sT, yrt_sinf(phi) * sT, cT));
       return spec_eval(c, wo, dg, *wi);
     }
   }
@@ -1800,7 +1819,7 @@ static void shade(const World* W, const Material* m, Medium cur, DG* dg, BSet* s
       float dc[4] = {m->transmission.x, m->transmission.y, m->transmission.z, 1.f};
       if (m->Kd >= 0) tex_get(B, m->Kd, m->ds[0] * dg->s + m->s0[0], m->ds[1] * dg->t + m->s0[1], dc);
       const V3 T = v3(dc[0] * m->transparency, dc[1] * m->transparency, dc[2] * m->transparency);
-      bs_add(s, B_THIN_TRANS, 0x01000000u, v3(logf(T.x), logf(T.y), logf(T.z)), 1.f * rcp(m->eta), m->thickness, 0);
+      bs_add(s, B_THIN_TRANS, 0x01000000u, v3(yrt_logf(T.x), yrt_logf(T.y), yrt_logf(T.z)), 1.f * rcp(m->eta), m->thickness, 0);
       break;
     }
     default: break;
@@ -1810,8 +1829,8 @@ static void shade(const World* W, const Material* m, Medium cur, DG* dg, BSet* s
 /* HDRILight::Le (lights/hdrilight.cpp:43-71) */
 static V3 hdri_Le(const World* W, const Light* L, V3 wo) {
   const V3 wi = xfmVector(L->w2l, neg(wo));
-  const float theta = acosf(clampf_(wi.y, -1.0f, 1.0f));
-  float phi = atan2f(-wi.z, -wi.x);
+  const float theta = yrt_acosf(clampf_(wi.y, -1.0f, 1.0f));
+  float phi = yrt_atan2f(-wi.z, -wi.x);
   if (phi < 0) phi += 2.0f * PI_F;
   const float u = 1.0f - (phi * ONE_OVER_TWO_PI_F), v = theta * ONE_OVER_PI_F;
   int x = (int)(u * L->w);
@@ -1942,10 +1961,10 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
         } else if (Lt->type == LT_DISTANT) { /* distantlight.h:46-50, shapesampler.h:149-165 */
           const float ang = Lt->halfAngle;
           const float phi = TWO_PI_F * S2X(0);
-          const float cT = 1.0f - S2Y(0) * (1.0f - cosf(ang));
+          const float cT = 1.0f - S2Y(0) * (1.0f - yrt_cosf(ang));
           const float sT = sqrtf(fmaxf(0.0f, 1.0f - cT * cT));
-          pdf = rcp(4.0f * PI_F * (sinf(0.5f * ang) * sinf(0.5f * ang)));
-          wi = lmul(frame_(Lt->D), v3(cosf(phi) * sT, sinf(phi) * sT, cT));
+          pdf = rcp(4.0f * PI_F * (yrt_sinf(0.5f * ang) * yrt_sinf(0.5f * ang)));
+          wi = lmul(frame_(Lt->D), v3(yrt_cosf(phi) * sT, yrt_sinf(phi) * sT, cT));
           Ls = Lt->L;
         }
         if (v3zero(Ls) || pdf == 0.f) continue;
@@ -1975,7 +1994,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     if (v3zero(c) || pdf <= 0.f) break;
     /* simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207) */
     if (!veq(medium.T, vs(1.0f)))
-      c = mulv(c, v3(powf(medium.T.x, h.t), powf(medium.T.y, h.t), powf(medium.T.z, h.t)));
+      c = mulv(c, v3(yrt_powf(medium.T.x, h.t), yrt_powf(medium.T.y, h.t), yrt_powf(medium.T.z, h.t)));
     if (type & 0xFFFF0000u) {
       const Material* mt = &W->mats[dg.material];
       if (mt->type == MT_DIELECTRIC) medium = med_eq(medium, mt->inside) ? mt->outside : mt->inside;
@@ -2071,7 +2090,7 @@ static void* worker(void* arg) {
         V3 L0 = muls(L, rcp((float)spp));
         if (J->gamma != 1.0f) {
           const float rg = rcp(J->gamma);
-          L0 = v3(powf(L0.x, rg), powf(L0.y, rg), powf(L0.z, rg));
+          L0 = v3(yrt_powf(L0.x, rg), yrt_powf(L0.y, rg), yrt_powf(L0.z, rg));
         }
         float* o = &J->out[((size_t)y * J->width + x) * 3];
         o[0] = L0.x; o[1] = L0.y; o[2] = L0.z;

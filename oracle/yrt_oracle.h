@@ -21,6 +21,10 @@
  *     Parity against Embree itself is unpinned (no Embree source or binary can run here).
  *   - C rand() in the shadow-ray jitter -> the counter hash hash_u01 (also used on the GPU).
  *   - SSE rcp/rsqrt approximations -> IEEE 1/x and 1/sqrt(x).
+ *   - the C runtime's sinf/cosf/powf/expf/logf/acosf/atanf/atan2f on the per-ray path (camera
+ *     rays, BRDF/light sampling, shading, resolve) -> the build's own yrt_libm.h
+ *     (yulio-raytracer_amd/csrc/common), evaluated with the same operations as the device does;
+ *     host-side setup (camera fov, sphere tessellation, HDRI tables) keeps glibc on both sides.
  *
  * Input: the "frame blob" written by yrtExportFrame (yulio-raytracer_amd/csrc/device/export.cpp)
  *   "YRTF" u32 version(1)
@@ -75,6 +79,8 @@ void oracle_random_ints(int seed, int n, int32_t* out);
 /* Random::getFloat (random.h:71), Permutation(size, rng) (permutation.h:42-48) `count` times
  * from one generator, vector_t::shuffle (vector.h:129-133) `count` times in place. */
 void oracle_random_floats(int seed, int n, float* out);
+/* yrt_libm.h functions (fn 0 sin 1 cos 2 exp 3 log 4 pow(x,y) 5 asin 6 acos 7 atan 8 atan2(x,y)) */
+void oracle_libm(int fn, int n, const float* x, const float* y, float* out);
 void oracle_permutations(int size, int seed, int count, int32_t* out);
 void oracle_shuffles(int n, int seed, int count, uint32_t* out);
 /* SamplerFactory::init sample table: dims as in the GPU table ([dim][set*spp+s]);

@@ -15,6 +15,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "yrt_libm.h"
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define YRT_HD __host__ __device__ __forceinline__
@@ -84,7 +86,7 @@ YRT_HD V3 mul(L3 a, V3 b) { return b.x * a.vx + b.y * a.vy + b.z * a.vz; }
 YRT_HD L3 mul(L3 a, L3 b) { return l3(mul(a, b.vx), mul(a, b.vy), mul(a, b.vz)); }
 YRT_HD L3 l3_rotate(V3 u_, float r) {
   V3 u = normalize(u_);
-  float s = sinf(r), c = cosf(r);
+  float s = yrt_sinf(r), c = yrt_cosf(r);  // shared with the per-ray stereo camera (yrt_libm.h)
   return l3_rows(u.x * u.x + (1 - u.x * u.x) * c, u.x * u.y * (1 - c) - u.z * s, u.x * u.z * (1 - c) + u.y * s,
                  u.x * u.y * (1 - c) + u.z * s, u.y * u.y + (1 - u.y * u.y) * c, u.y * u.z * (1 - c) - u.x * s,
                  u.x * u.z * (1 - c) - u.y * s, u.y * u.z * (1 - c) + u.x * s, u.z * u.z + (1 - u.z * u.z) * c);

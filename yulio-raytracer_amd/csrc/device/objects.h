@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -147,6 +148,9 @@ struct GpuScene;  // scene_gpu.h
 struct SceneObj : Object {
   std::vector<std::shared_ptr<ScenePrim>> slots;
   std::shared_ptr<GpuScene> gpu;
+  // copies of `gpu` on the other HIP devices of a multi-GPU device (by HIP device id),
+  // re-made when the scene is rebuilt or refit (device.cpp scene_on)
+  std::map<int, std::shared_ptr<GpuScene>> replicas;
   explicit SceneObj(const std::string& t) : Object(Kind::SCENE, t) {}
   void commit() override;
 };

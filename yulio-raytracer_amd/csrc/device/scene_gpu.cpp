@@ -16,6 +16,27 @@
 
 namespace yrt {
 
+// SceneView pointers of the scene's own device buffers (counts already set in S.view)
+static void bind_view(GpuScene& S) {
+  SceneView& v = S.view;
+  v.nodes = S.nodes.as<GpuNode>();
+  v.tris = S.tris.as<GpuTri>();
+  v.triGeom = S.triGeom.as<int>();
+  v.indices = S.indices.as<int4>();
+  v.positions = S.positions.as<float4>();
+  v.normals = S.normals.as<float4>();
+  v.texcoords = S.texcoords.as<float2>();
+  v.geoms = S.geoms.as<GpuGeom>();
+  v.materials = S.materials.as<GpuMaterial>();
+  v.textures = S.textures.as<GpuTexture>();
+  v.images = S.images.as<GpuImage>();
+  v.texels = S.texels.as<uint8_t>();
+  v.lights = S.lights.as<GpuLight>();
+  v.envLights = S.envLights.as<int>();
+  v.media = S.media.as<float4>();
+  v.hdriDist = nullptr;
+}
+
 std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<ScenePrim>>& prims, int stackDepth,
                                           bool upload) {
   auto t0 = std::chrono::steady_clock::now();
@@ -236,27 +257,11 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->envLights.upload(envLights);
   S->media.upload(media);
 
-  SceneView& v = S->view;
-  v.nodes = S->nodes.as<GpuNode>();
-  v.tris = S->tris.as<GpuTri>();
-  v.triGeom = S->triGeom.as<int>();
-  v.indices = S->indices.as<int4>();
-  v.positions = S->positions.as<float4>();
-  v.normals = S->normals.as<float4>();
-  v.texcoords = S->texcoords.as<float2>();
-  v.geoms = S->geoms.as<GpuGeom>();
-  v.materials = S->materials.as<GpuMaterial>();
-  v.textures = S->textures.as<GpuTexture>();
-  v.images = S->images.as<GpuImage>();
-  v.texels = S->texels.as<uint8_t>();
-  v.lights = S->lights.as<GpuLight>();
-  v.envLights = S->envLights.as<int>();
-  v.media = S->media.as<float4>();
-  v.hdriDist = nullptr;
-  v.numLights = (int)lights.size();
-  v.numEnvLights = (int)envLights.size();
-  v.numNodes = (int)bvh.nodes.size();
-  v.numTris = gidBase;
+  S->view.numLights = (int)lights.size();
+  S->view.numEnvLights = (int)envLights.size();
+  S->view.numNodes = (int)bvh.nodes.size();
+  S->view.numTris = gidBase;
+  bind_view(*S);
 
   // refit support: slot -> geometry, gid -> leaf position, nodes grouped by depth
   S->slotsCommitted = prims;
@@ -300,6 +305,42 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->hTriGeom = triGeom;
   S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return S;
+}
+
+std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
+  HIP_CHECK(hipSetDevice(device));
+  auto R = std::make_shared<GpuScene>();
+  R->device = device;
+  R->serial = src.serial;  // same committed scene: the sample-table caches may key on it
+  auto copy = [&](DevBuf& dst, const DevBuf& from) {
+    if (!from.p) return;
+    dst.alloc(from.bytes);
+    HIP_CHECK(hipMemcpyPeer(dst.p, device, from.p, src.device, from.bytes));
+  };
+  copy(R->nodes, src.nodes);
+  copy(R->tris, src.tris);
+  copy(R->triGeom, src.triGeom);
+  copy(R->indices, src.indices);
+  copy(R->positions, src.positions);
+  copy(R->normals, src.normals);
+  copy(R->texcoords, src.texcoords);
+  copy(R->geoms, src.geoms);
+  copy(R->materials, src.materials);
+  copy(R->textures, src.textures);
+  copy(R->images, src.images);
+  copy(R->texels, src.texels);
+  copy(R->lights, src.lights);
+  copy(R->envLights, src.envLights);
+  copy(R->media, src.media);
+  R->view = src.view;
+  bind_view(*R);
+  R->materialMask = src.materialMask;
+  R->precomputed = src.precomputed;
+  R->numTris = src.numTris;
+  R->numGeoms = src.numGeoms;
+  R->bvhDepth = src.bvhDepth;
+  R->refits = src.refits;
+  return R;
 }
 
 bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>& prims, hipStream_t stream) {

@@ -84,6 +84,9 @@ struct GpuScene {
 
 std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<ScenePrim>>& prims, int stackDepth,
                                           bool upload);
+// A copy of an uploaded scene's device buffers on another HIP device (peer copies over xGMI),
+// for multi-GPU tile rendering; the host-side mirrors stay with the source.
+std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device);
 // Commits `prims` onto an uploaded scene without a rebuild when only vertex positions/normals
 // of some primitives changed (faceCamera re-orientation): uploads the moved vertices and
 // refits the BVH on the GPU. Returns false (scene untouched) when a rebuild is needed.

@@ -161,7 +161,7 @@ __device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3
     const float lensRadius = cam.xyzStraight[0], focalDistance = cam.xyzStraight[1];
     // uniformSampleDisk (samplers/shapesampler.h:187-191)
     const float r = sqrtf(lx), theta = kTwoPi * ly;
-    const V3 begin = xfmPoint(l2w, v3(lensRadius * r * cosf(theta), lensRadius * r * sinf(theta), 0.0f));
+    const V3 begin = xfmPoint(l2w, v3(lensRadius * r * yrt_cosf(theta), lensRadius * r * yrt_sinf(theta), 0.0f));
     const V3 end = p2w.p + focalDistance * (fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
     org = begin;
     dir = normalize(end - begin);
@@ -176,17 +176,17 @@ __device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3
   float absoluteVerticalAngle = 0.f;
   if (eyeCubeFaceIndex <= 3) {
     const V3 xDir = normalize(fx * pixel2world.l.vx + .5f * pixel2world.l.vy + pixel2world.l.vz);
-    theta = acosf(clampf(dot(xDir, xyzStraight), -1.f, 1.f)) * signf_(fx - .5f);
+    theta = yrt_acosf(clampf(dot(xDir, xyzStraight), -1.f, 1.f)) * signf_(fx - .5f);
     const V3 yDir = normalize(.5f * pixel2world.l.vx + yPixel * pixel2world.l.vy + pixel2world.l.vz);
-    const float yAngle = rad2deg(acosf(clampf(dot(yDir, xyzStraight), -1.f, 1.f))) * signf_(yPixel - .5f);
+    const float yAngle = rad2deg(yrt_acosf(clampf(dot(yDir, xyzStraight), -1.f, 1.f))) * signf_(yPixel - .5f);
     absoluteVerticalAngle = fabsf(yAngle);
   } else {
     const V3 xyDir = v3(fx - .5f, yPixel - .5f, 0.f);
     const V3 xyDirNorm = normalize(xyDir);
     const V3 xyUp = v3(0.f, eyeCubeFaceIndex == 4 ? -1.f : 1.f, 0.f);
-    theta = acosf(clampf(dot(xyDirNorm, xyUp), -1.f, 1.f)) * signf_(fx - .5f);
+    theta = yrt_acosf(clampf(dot(xyDirNorm, xyUp), -1.f, 1.f)) * signf_(fx - .5f);
     const V3 xyzDir = normalize(fx * pixel2world.l.vx + yPixel * pixel2world.l.vy + pixel2world.l.vz);
-    const float xyzAngle = rad2deg(acosf(clampf(dot(xyzDir, xyzStraight), -1.f, 1.f)));
+    const float xyzAngle = rad2deg(yrt_acosf(clampf(dot(xyzDir, xyzStraight), -1.f, 1.f)));
     absoluteVerticalAngle = 90.f - fabsf(xyzAngle);
   }
   float eyeOffset = cam.eyeSeparation * (cam.cubeFaceIndex < 6 ? -.5f : .5f);
@@ -199,7 +199,7 @@ __device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3
   const A3 rayRotationSpace = a3_rotate_about(origin, up, theta);
   const V3 rayOrigin = mul(rayRotationSpace, p2w).p;
   if (cam.toeIn) {
-    const float toeInCorrection = -atanf(eyeOffset * cam.rcpZeroParallaxDistance);
+    const float toeInCorrection = -yrt_atanf(eyeOffset * cam.rcpZeroParallaxDistance);
     p2w = mul(a3_rotate_about(rayOrigin, up, toeInCorrection), p2w);
   }
   org = rayOrigin;
@@ -778,7 +778,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
         tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
       const float tr = m.p[9];
       const V3 T = v3(dc[0] * tr, dc[1] * tr, dc[2] * tr);
-      add_comp(bs, C_THIN_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3(logf(T.x), logf(T.y), logf(T.z)), m.p[10],
+      add_comp(bs, C_THIN_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3(yrt_logf(T.x), yrt_logf(T.y), yrt_logf(T.z)), m.p[10],
                m.p[8]);
       break;
     }
@@ -795,8 +795,8 @@ __device__ __forceinline__ void img_get(const SceneView& sv, int image, int x, i
 __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
   const A3 w2l = ldA3(lt.w2l);
   const V3 wi = xfmVector(w2l, -wo);
-  const float theta = acosf(clampf(wi.y, -1.0f, 1.0f));
-  float phi = atan2f(-wi.z, -wi.x);
+  const float theta = yrt_acosf(clampf(wi.y, -1.0f, 1.0f));
+  float phi = yrt_atan2f(-wi.z, -wi.x);
   if (phi < 0) phi += 2.0f * kPi;
   const float u = 1.0f - (phi * kOneOverTwoPi);
   const float v = theta * kOneOverPi;
@@ -890,10 +890,10 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
   if ((LM & (1u << LIGHT_DISTANT)) && lt.type == LIGHT_DISTANT) {  // distantlight.h:46-50, uniformSampleCone (shapesampler.h:149-165)
     const float angle = lt.bsphere[0];
     const float phi = kTwoPi * sx;
-    const float cosTheta = 1.0f - sy * (1.0f - cosf(angle));
+    const float cosTheta = 1.0f - sy * (1.0f - yrt_cosf(angle));
     const float sinTheta = cos2sin(cosTheta);
-    const V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
-    pdf = rcpf_(4.0f * kPi * sqrf(sinf(0.5f * angle)));
+    const V3 l = v3(yrt_cosf(phi) * sinTheta, yrt_sinf(phi) * sinTheta, cosTheta);
+    pdf = rcpf_(4.0f * kPi * sqrf(yrt_sinf(0.5f * angle)));
     wi = mul(frame(ld3(lt.e1)), l);
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
@@ -1019,7 +1019,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
           if (MM & mat_bit(MAT_DIELECTRIC)) {
             // simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207)
             const float4 T = sv.media[medium];
-            if (!(T.x == 1.f && T.y == 1.f && T.z == 1.f)) c = c * v3(powf(T.x, h.x), powf(T.y, h.x), powf(T.z, h.x));
+            if (!(T.x == 1.f && T.y == 1.f && T.z == 1.f)) c = c * v3(yrt_powf(T.x, h.x), yrt_powf(T.y, h.x), yrt_powf(T.z, h.x));
             if ((type & BT_TRANSMISSION) && dg.material >= 0) {
               const GpuMaterial& mt = sv.materials[dg.material];
               if (mt.type == MAT_DIELECTRIC) medium = medium == mt.media[1] ? mt.media[0] : mt.media[1];
@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
     }
     accu[pix] = a;
     V3 L0 = accumulate ? v3(a.x, a.y, a.z) * rcpf_(a.w) : L * rcpf_((float)rp.spp);
-    if (rp.gamma != 1.0f) L0 = v3(powf(L0.x, rp.rcpGamma), powf(L0.y, rp.rcpGamma), powf(L0.z, rp.rcpGamma));
+    if (rp.gamma != 1.0f) L0 = v3(yrt_powf(L0.x, rp.rcpGamma), yrt_powf(L0.y, rp.rcpGamma), yrt_powf(L0.z, rp.rcpGamma));
     if (fbFloat) {
       float* o = fbFloat + ((size_t)y * rp.width + x) * 3;
       o[0] = L0.x;
@@ -1334,6 +1334,67 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(k_resolve_pixels, dim3(grid_for(bi.numPixels, YRT_BLOCK, 8192)), dim3(YRT_BLOCK), 0, s, fv, pb, bi,
                      fbFloat, fbRGB8, rgb8Stride, accu, accumulate);
+}
+
+// ---------------------------------------------------------------- multi-GPU tile slabs
+__device__ __forceinline__ bool slab_pixel(int width, int height, int tileOffset, int tileStride, int i, int& x,
+                                           int& y) {
+  const int ntx = (width + 15) >> 4;
+  const int t = tileOffset + (i >> 8) * tileStride;
+  x = (t % ntx) * 16 + (i & 15);
+  y = (t / ntx) * 16 + ((i >> 4) & 15);
+  return x < width && y < height;
+}
+
+__global__ __launch_bounds__(256) void k_pack_tiles(const float* __restrict__ fbFloat,
+                                                    const uint8_t* __restrict__ fbRGB8, int width, int height,
+                                                    int rgb8Stride, int tileOffset, int tileStride, int n,
+                                                    float4* __restrict__ slab) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int x, y;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (slab_pixel(width, height, tileOffset, tileStride, i, x, y)) {
+      const float* f = fbFloat + ((size_t)y * width + x) * 3;
+      const uint8_t* c = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
+      v = make_float4(f[0], f[1], f[2], __uint_as_float((unsigned)c[0] | ((unsigned)c[1] << 8) | ((unsigned)c[2] << 16)));
+    }
+    slab[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_tiles(const float4* __restrict__ slab, float* __restrict__ fbFloat,
+                                                      uint8_t* __restrict__ fbRGB8, int width, int height,
+                                                      int rgb8Stride, int tileOffset, int tileStride, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int x, y;
+    if (!slab_pixel(width, height, tileOffset, tileStride, i, x, y)) continue;
+    const float4 v = slab[i];
+    float* f = fbFloat + ((size_t)y * width + x) * 3;
+    f[0] = v.x;
+    f[1] = v.y;
+    f[2] = v.z;
+    const unsigned c = __float_as_uint(v.w);
+    uint8_t* o = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
+    o[0] = (uint8_t)(c & 255u);
+    o[1] = (uint8_t)((c >> 8) & 255u);
+    o[2] = (uint8_t)((c >> 16) & 255u);
+  }
+}
+
+void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, int width, int height, int rgb8Stride,
+                       int tileOffset, int tileStride, int numTiles, float4* slab, hipStream_t s) {
+  const int n = numTiles * 256;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_tiles, dim3((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384), dim3(256), 0, s, fbFloat, fbRGB8, width,
+                     height, rgb8Stride, tileOffset, tileStride, n, slab);
+}
+
+void launch_unpack_tiles(const float4* slab, float* fbFloat, uint8_t* fbRGB8, int width, int height, int rgb8Stride,
+                         int tileOffset, int tileStride, int numTiles, hipStream_t s) {
+  const int n = numTiles * 256;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_unpack_tiles, dim3((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384), dim3(256), 0, s, slab, fbFloat, fbRGB8,
+                     width, height, rgb8Stride, tileOffset, tileStride, n);
 }
 
 // SingleRayDevice::rtPick (api/singleray_device.cpp:692-708): one camera ray at image-plane

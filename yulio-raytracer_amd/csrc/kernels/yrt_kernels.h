@@ -127,6 +127,14 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
 int trace_profile(unsigned long long* out8, int reset);
+// Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (image tile =
+// tileOffset + j * tileStride, j < numTiles) as a slab of numTiles * 256 float4 (rgb float,
+// w = the RGB8 bytes), in tile order j and scan order within the tile; unpack scatters a slab
+// back into the frame. Pixels outside the image are zero in the slab and skipped on unpack.
+void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, int width, int height, int rgb8Stride,
+                       int tileOffset, int tileStride, int numTiles, float4* slab, hipStream_t s);
+void launch_unpack_tiles(const float4* slab, float* fbFloat, uint8_t* fbRGB8, int width, int height, int rgb8Stride,
+                         int tileOffset, int tileStride, int numTiles, hipStream_t s);
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s);
 // BVH refit after faceCamera updates: rewrite triangles [firstTri, firstTri+numTris) (global
 // ids) from the vertex buffer in every leaf slot that references them (leafSlots[leafStart[g]

@@ -129,7 +129,7 @@ __device__ __forceinline__ V3 reflect2(V3 V, V3 N) { return reflect3(V, N, dot(V
 __device__ __forceinline__ V3 cosine_hemi(float u, float v, V3 N, float& pdf) {
   const float phi = kTwoPi * u;
   const float cosTheta = sqrtf(v), sinTheta = sqrtf(1.0f - v);
-  V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
+  V3 l = v3(yrt_cosf(phi) * sinTheta, yrt_sinf(phi) * sinTheta, cosTheta);
   pdf = cosTheta * kOneOverPi;
   return mul(frame(N), l);
 }
@@ -234,7 +234,7 @@ __device__ __forceinline__ float aniso_D(float nx, float ny, const DG& dg, V3 wh
   const float R = sqrf(cosPhiH) + sqrf(sinPhiH);
   if (R == 0.0f) return norm2;
   const float n = (nx * sqrf(cosPhiH) + ny * sqrf(sinPhiH)) * rcpf_(R);
-  return norm2 * powf(fabsf(cosThetaH), n);
+  return norm2 * yrt_powf(fabsf(cosThetaH), n);
 }
 
 // Microfacet<Fresnel, Distribution>::eval (brdfs/microfacet.h:28-41) for the dielectric /
@@ -266,7 +266,7 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* 
   } else {
     const float n = diel ? c.c : c.a;
     const float norm2 = (n + 2) * kOneOverTwoPi;
-    D = norm2 * powf(fabsf(dot(wh, dg.Ns)), n);
+    D = norm2 * yrt_powf(fabsf(dot(wh, dg.Ns)), n);
   }
   const float G = fminf(fminf(1.0f, 2.0f * cosThetaH * cosThetaO * rcpf_(cosTheta)),
                         2.0f * cosThetaH * cosThetaI * rcpf_(cosTheta));
@@ -276,14 +276,14 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* 
 // Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26)
 __device__ __forceinline__ V3 minnaert_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   const float cosThetaI = clampf(dot(wi, dg.Ns));
-  const float backScatter = powf(clampf(dot(wo, wi)), c.a);
+  const float backScatter = yrt_powf(clampf(dot(wo, wi)), c.a);
   return c.R * backScatter * cosThetaI / kPi;
 }
 __device__ __forceinline__ V3 velvety_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   const float cosThetaO = clampf(dot(wo, dg.Ns));
   const float cosThetaI = clampf(dot(wi, dg.Ns));
   const float sinThetaO = sqrtf(1.0f - cosThetaO * cosThetaO);
-  const float horizonScatter = powf(sinThetaO, c.a);
+  const float horizonScatter = yrt_powf(sinThetaO, c.a);
   return c.R * horizonScatter * cosThetaI / kPi;
 }
 
@@ -305,7 +305,7 @@ __device__ __forceinline__ V3 layer_eval(const Comp& c, V3 wo, const DG& dg, V3 
 __device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   V3 r = reflect2(wo, dg.Ns);
   if (dot(r, wi) < 0) return v3s(0.0f);
-  return c.R * (c.a + 2) * (1.0f / (2.0f * kPi)) * powf(dot(r, wi), c.a) * clampf(dot(wi, dg.Ns));
+  return c.R * (c.a + 2) * (1.0f / (2.0f * kPi)) * yrt_powf(dot(r, wi), c.a) * clampf(dot(wi, dg.Ns));
 }
 
 template <unsigned CM>
@@ -360,7 +360,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float alpha = c.b * rcpf_(cosTheta);
       float cosThetaT;
       V3 la = c.R * alpha;
-      return v3(expf(la.x), expf(la.y), expf(la.z)) * (1.f - fresnel2(cosTheta, c.a, &cosThetaT));
+      return v3(yrt_expf(la.x), yrt_expf(la.y), yrt_expf(la.z)) * (1.f - fresnel2(cosTheta, c.a, &cosThetaT));
     }
     case C_DIEL_LAYER_LAMB: {
       pdf = 0.0f;
@@ -390,12 +390,12 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float n = c.c;
       const float norm1 = (n + 1) * kOneOverTwoPi;
       const float phi = kTwoPi * sx;
-      const float cosPhi = cosf(phi);
-      const float sinPhi = sinf(phi);
-      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float cosPhi = yrt_cosf(phi);
+      const float sinPhi = yrt_sinf(phi);
+      const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
       const float sinTheta = cos2sin(cosTheta);
       V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
-      float whpdf = norm1 * powf(cosTheta, n);
+      float whpdf = norm1 * yrt_powf(cosTheta, n);
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
@@ -408,12 +408,12 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float n = c.a;
       const float norm1 = (n + 1) * kOneOverTwoPi;
       const float phi = kTwoPi * sx;
-      const float cosPhi = cosf(phi);
-      const float sinPhi = sinf(phi);
-      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float cosPhi = yrt_cosf(phi);
+      const float sinPhi = yrt_sinf(phi);
+      const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
       const float sinTheta = cos2sin(cosTheta);
       V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
-      float whpdf = norm1 * powf(cosTheta, n);
+      float whpdf = norm1 * yrt_powf(cosTheta, n);
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
       if (dot(wi, dg.Ns) <= 0.0f) return v3s(0.0f);
@@ -426,15 +426,15 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float nx = c.a, ny = c.b;
       const float norm1 = sqrtf((nx + 1) * (ny + 1)) * kOneOverTwoPi;
       const float phi = kTwoPi * sx;
-      const float sinPhi0 = sqrtf(nx + 1) * sinf(phi);
-      const float cosPhi0 = sqrtf(ny + 1) * cosf(phi);
+      const float sinPhi0 = sqrtf(nx + 1) * yrt_sinf(phi);
+      const float cosPhi0 = sqrtf(ny + 1) * yrt_cosf(phi);
       const float nrm = rsqrtf_(sqrf(sinPhi0) + sqrf(cosPhi0));
       const float sinPhi = sinPhi0 * nrm;
       const float cosPhi = cosPhi0 * nrm;
       const float n = nx * sqrf(cosPhi) + ny * sqrf(sinPhi);
-      const float cosTheta = powf(sy, rcpf_(n + 1));
+      const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
       const float sinTheta = cos2sin(cosTheta);
-      const float whpdf = norm1 * powf(cosTheta, n);
+      const float whpdf = norm1 * yrt_powf(cosTheta, n);
       const V3 h = v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta);
       const V3 wh = h.x * dg.Tx + h.y * dg.Ty + h.z * dg.Ns;
       wi = reflect2(wo, wh);
@@ -475,10 +475,10 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       // powerCosineSampleHemisphere(s.x, s.y, reflect(wo, Ns), exp) (shapesampler.h:104-121)
       const float e = c.a;
       const float phi = kTwoPi * sx;
-      const float cosTheta = powf(sy, rcpf_(e + 1));
+      const float cosTheta = yrt_powf(sy, rcpf_(e + 1));
       const float sinTheta = cos2sin(cosTheta);
-      V3 l = v3(cosf(phi) * sinTheta, sinf(phi) * sinTheta, cosTheta);
-      pdf = (e + 1.0f) * powf(cosTheta, e) * kOneOverTwoPi;
+      V3 l = v3(yrt_cosf(phi) * sinTheta, yrt_sinf(phi) * sinTheta, cosTheta);
+      pdf = (e + 1.0f) * yrt_powf(cosTheta, e) * kOneOverTwoPi;
       wi = mul(frame(reflect2(wo, dg.Ns)), l);
       return specular_eval(c, wo, dg, wi);
     }
