@@ -5,10 +5,11 @@ Uber + Sponza JPEG textures, dome light 8 8 8), 2048x2048, 64 spp, depth 10,
 tMaxShadowRay 120, camera of models/test_stereo_view.ecs:2-10.
 
 One step = one full frame (all W*H*spp paths to termination) rendered through the C ABI
-(yrtRenderFrame), scene resident in HBM. With N GPUs (torch.distributed, one process per
-GPU) the frame's 16x16 tiles are dealt round-robin over the ranks, each rank
-renders its shard, and the RGB8 shards are combined on rank 0 with one RCCL reduce
-(disjoint supports, so the sum is a gather) inside the step.
+(yrtRenderFrame), scene resident in HBM. With N GPUs (torch.distributed launches one process
+per GPU) the frame's 16x16 tiles are dealt round-robin over the ranks, each
+rank renders its shard, and the device plugin gathers the tiles on rank 0 inside
+rtRenderFrame with its own RCCL communicator (yrtSetShardComm: grouped send/recv of tile
+slabs over xGMI); see setup_gather for the fallback.
 
 Weak scaling: at N GPUs one step is N progressive iterations of that frame (AccuBuffer
 accumulation, integratorrenderer.cpp:166), all tiles of all N iterations dealt round-robin;
@@ -87,6 +88,7 @@ def main():
     R, S, T, F = info["renderer"], info["scene"], info["tonemapper"], info["framebuffer"]
     sinfo = dev.scene_info(S)
     dev.set_tile_shard(rank, world)
+    gather = setup_gather(dev, rank, world, backend) if world > 1 else "single GPU"
     if a.capacity:
         dev.set_batch_capacity(a.capacity)
 
@@ -111,7 +113,7 @@ def main():
             dev.rtRenderFrame(R, cam, S, T, F, 1 if k else 0)
             s_k = dev.render_stats()
             st = s_k if st is None else {n: st[n] + s_k[n] for n in st}
-        if world > 1:
+        if world > 1 and not gather.startswith("C++"):
             import ctypes
             p = dev.rtMapFrameBuffer(F)
             host = np.ctypeslib.as_array((ctypes.c_uint8 * fb_t.numel()).from_address(p))
@@ -153,7 +155,7 @@ def main():
     rays, closest, shadow = tot.tolist()
     elapsed = tmax.item()
 
-    stereo = stereo_cubemap(a, dev, rank, world, backend) if a.stereo_frames > 0 else None
+    stereo = stereo_cubemap(a, dev, rank, world, backend, gather) if a.stereo_frames > 0 else None
 
     if rank == 0:
         # dominant trace kernel: what binds it. The BVH and the
@@ -215,6 +217,7 @@ def main():
             "rays_closest": closest, "rays_shadow": shadow,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "gather": gather,
             "stereo_cubemap": stereo,
         }
         print(json.dumps(out), flush=True)
@@ -222,6 +225,34 @@ def main():
     dev.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def setup_gather(dev, rank, world, backend):
+    """The frame gather of an N-rank run: the device plugin's own RCCL communicator (rank 0's
+    ncclGetUniqueId broadcast over torch.distributed, then yrtSetShardComm): every rtRenderFrame
+    ends with each rank's tile slab sent to rank 0 over xGMI (grouped send/recv) — the C++
+    product path. If that communicator cannot be formed on every rank (e.g. the gloo rehearsal
+    with several ranks on one GPU, which RCCL refuses), the run falls back to one
+    torch.distributed reduce of the RGB8 frames (disjoint tiles) and says so."""
+    import torch
+    import torch.distributed as dist
+    dd = "cuda" if backend == "nccl" else "cpu"
+    err = "" if backend == "nccl" else f"backend {backend}"
+    uid = None
+    if not err:
+        try:  # every rank first checks that librccl loads (a rank failing inside the
+            uid = dev.shard_comm_unique_id()  # collective ncclCommInitRank would hang the others)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            err = str(e)[:200]
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dd)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() == 1:
+        box = [uid if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        dev.set_shard_comm(rank, world, box[0])
+        return "C++ RCCL gather to rank 0 inside rtRenderFrame (yrtSetShardComm)"
+    dev.set_tile_shard(rank, world)
+    return f"torch.distributed reduce of RGB8 frames (C++ RCCL comm unavailable: {err or 'on another rank'})"
 
 
 def workload_config(a, sinfo, world):
@@ -304,7 +335,7 @@ def cpu_info():
             "cgroup_cpu_quota": quota}
 
 
-def stereo_cubemap(a, dev, rank, world, backend):
+def stereo_cubemap(a, dev, rank, world, backend, gather):
     """BASELINE.json configs[3]: the test_stereo stereo cubemap (12 faces x 1536^2, 256 spp,
     depth 10, test_stereo_view.ecs), every face's 16x16 tiles dealt round-robin over the
     ranks, the faceCamera billboard refit per face, and one RCCL reduce of the
@@ -316,7 +347,6 @@ def stereo_cubemap(a, dev, rank, world, backend):
     scenes = ROOT / "scenes"
     ses = yrt.Session(["-i", str(scenes / "test_stereo.xml"), "-c", str(scenes / "test_stereo_view.ecs"),
                        "-size", "1536", "1536", "-spp", "256", "-stereo"], device=dev)
-    dev.set_tile_shard(rank, world)
     info = ses.info()
     W, H = info["width"], info["height"]
     stride = (3 * W + 3) // 4 * 4
@@ -333,7 +363,7 @@ def stereo_cubemap(a, dev, rank, world, backend):
             st = dev.render_stats()
             rays += st["raysClosest"] + st["raysShadow"]
             faces[f, :img.size].copy_(torch.from_numpy(np.ascontiguousarray(img).reshape(-1)))
-        if world > 1:
+        if world > 1 and not gather.startswith("C++"):
             dist.reduce(faces, dst=0, op=dist.ReduceOp.SUM)
     if world > 1:
         dist.barrier()
@@ -346,7 +376,6 @@ def stereo_cubemap(a, dev, rank, world, backend):
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
     ses.close()
-    dev.set_tile_shard(0, 1)
     dt = tm.item()
     samples = 12.0 * W * H * 256 * a.stereo_frames
     return {"metric": "Mrays/s (test_stereo stereo cubemap 12x1536^2 256spp, closest+shadow queries)",

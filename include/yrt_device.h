@@ -39,6 +39,10 @@ typedef void* YRTHandle;
  * CPU test suite. numThreads / threadsPriority are accepted
  * for signature parity (they size the CPU TaskScheduler in the reference and are unused
  * on the GPU). */
+/* parms: "" or "device=<k>": one HIP device; "devices=<a,b,...>" / "devices=all": the frame's
+ * 16x16 tiles are dealt round-robin over several HIP devices, one host
+ * thread each, and gathered on the first (RCCL over xGMI between distinct GPUs; an id may
+ * repeat for logical shards of one GPU); "host": no GPU (loaders, BVH, frame export). */
 YRT_API YRTDevice yrtNewDevice(const char* parms, size_t numThreads, int threadsPriority, const char* rtcore_cfg);
 YRT_API void yrtDeleteDevice(YRTDevice dev);
 YRT_API const char* yrtGetLastError(YRTDevice dev);
@@ -169,8 +173,20 @@ YRT_API int64_t yrtExportFrame(YRTDevice dev, YRTHandle renderer, YRTHandle came
 YRT_API int yrtSetFrameSeed(YRTDevice dev, uint32_t seed);
 /* Paths in flight per wavefront batch (default 64M, ~10 GB of wavefront state); smaller for tests. */
 YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
-/* Tile sharding for multi-GPU: render only tiles with (tileIndex % count) == index. */
+/* Tile sharding across processes: this process renders only the tiles with
+ * (tileIndex % count) == index (dealt further over its own HIP devices, see yrtNewDevice);
+ * without a communicator (yrtSetShardComm) the other tiles' pixels are left zero. */
 YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
+/* Multi-GPU, one process per GPU (the reference's device_network image split,
+ * devices/device_network/network_device.cpp:255-300, as an RCCL gather over xGMI):
+ * yrtShardCommUniqueId fills 128 bytes on rank 0 (ncclGetUniqueId), which the caller
+ * broadcasts; every rank then calls yrtSetShardComm with it. Tiles are dealt round-robin
+ * (tile % world == rank) and every rtRenderFrame ends with a grouped RCCL send of each rank's
+ * tile slab to rank 0, whose framebuffer then holds the whole frame. */
+YRT_API int yrtShardCommUniqueId(void* id128);
+YRT_API int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128);
+/* HIP devices (logical shards) this device renders on (yrtNewDevice "devices=..."). */
+YRT_API int yrtGetDeviceCount(YRTDevice dev);
 /* Scene commits that only move the vertices of some primitives (faceCamera re-orientation by
  * rtUpdatePrimitive, the FPR loop of renderer.cpp:550-559) refit the BVH on the GPU instead of
  * rebuilding it (on by default). yrtGetSceneRefits: refit commits since the last rebuild. */

@@ -41,6 +41,8 @@ def _sig(name, res, *args):
 
 _sig("oracle_render", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, vp, C.POINTER(OracleStats))
 _sig("oracle_trace", i32, vp, sz, vp, vp, i32, i32, vp)
+_sig("oracle_render_shard", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, i32, i32, vp,
+     C.POINTER(OracleStats))
 _sig("oracle_count_visits", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
      C.POINTER(C.c_double), vp, sz)
 _sig("oracle_random_ints", None, i32, i32, vp)
@@ -69,6 +71,18 @@ def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0):
                             C.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle_render: {_err()}")
+    return out, {n: getattr(st, n) for n, _ in st._fields_}
+
+
+def render_shard(blob: bytes, width, height, gamma, index, count, threads=0):
+    """The tiles t % count == index of the frame (SURVEY §8(e) split); other pixels NaN."""
+    threads = threads or cpu_count()
+    out = np.full((height, width, 3), np.nan, np.float32)
+    st = OracleStats()
+    rc = _lib.oracle_render_shard(blob, len(blob), width, height, gamma, 0, 0, width, height, index, count, threads,
+                                  out.ctypes.data, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_shard: {_err()}")
     return out, {n: getattr(st, n) for n, _ in st._fields_}
 
 

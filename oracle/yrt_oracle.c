@@ -2049,6 +2049,7 @@ typedef struct {
   const Camera* C;
   const uint8_t* sets;
   int width, height, x0, y0, x1, y1, ntx, nty;
+  int shardIndex, shardCount; /* only tiles with tile % shardCount == shardIndex */
   float gamma;
   uint32_t seed;
   float* out;
@@ -2065,6 +2066,7 @@ static void* worker(void* arg) {
   for (;;) {
     const int tile = __sync_fetch_and_add(&J->next, 1);
     if (tile >= J->ntx * J->nty) break;
+    if (tile % J->shardCount != J->shardIndex) continue;
     const int tx = (tile % J->ntx) * 16, ty = (tile / J->ntx) * 16;
     for (int dy = 0; dy < 16; dy++) {
       const int y = ty + dy;
@@ -2158,6 +2160,12 @@ static void debug_render(const World* W, const RCfg* R, const Camera* C, int wid
 
 int oracle_render(const void* blob, size_t bytes, int width, int height, float gamma, int x0, int y0, int x1, int y1,
                   int threads, float* out, OracleStats* stats) {
+  return oracle_render_shard(blob, bytes, width, height, gamma, x0, y0, x1, y1, 0, 1, threads, out, stats);
+}
+
+int oracle_render_shard(const void* blob, size_t bytes, int width, int height, float gamma, int x0, int y0, int x1,
+                        int y1, int shardIndex, int shardCount, int threads, float* out, OracleStats* stats) {
+  if (shardCount < 1 || shardIndex < 0 || shardIndex >= shardCount) return -1;
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   Blob B;
@@ -2185,6 +2193,7 @@ int oracle_render(const void* blob, size_t bytes, int width, int height, float g
   J.x0 = x0 < 0 ? 0 : x0; J.y0 = y0 < 0 ? 0 : y0;
   J.x1 = x1 <= 0 || x1 > width ? width : x1; J.y1 = y1 <= 0 || y1 > height ? height : y1;
   J.ntx = (width + 15) / 16; J.nty = (height + 15) / 16;
+  J.shardIndex = shardIndex; J.shardCount = shardCount;
   J.gamma = gamma;
   J.seed = B.seed;
   J.out = out;

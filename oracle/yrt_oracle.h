@@ -61,6 +61,11 @@ typedef struct OracleStats {
 int oracle_render(const void* blob, size_t bytes, int width, int height, float gamma, int x0, int y0, int x1, int y1,
                   int threads, float* out_rgb, OracleStats* stats);
 
+/* oracle_render restricted to the 16x16 tiles with tile % shardCount == shardIndex (the
+ * multi-GPU tile split of SURVEY §8(e)); other pixels are left untouched. */
+int oracle_render_shard(const void* blob, size_t bytes, int width, int height, float gamma, int x0, int y0, int x1,
+                        int y1, int shardIndex, int shardCount, int threads, float* out_rgb, OracleStats* stats);
+
 /* Traces rays against the blob's scene: org4/dir4 as in yrtIntersect; hit4 = (t,u,v,tri)
  * (tri as int bits, -1 miss). anyHit != 0 -> occluded test, hit4.w = 1/0. */
 int oracle_trace(const void* blob, size_t bytes, const float* org4, const float* dir4, int n, int anyHit,

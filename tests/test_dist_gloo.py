@@ -1,5 +1,8 @@
 """world_size-2 gloo rehearsal of the multi-GPU path on CPU: tile shards are
-disjoint and complete, and gather_frame reassembles the frame exactly on rank 0."""
+disjoint and complete; each rank renders only its tiles (the oracle's tile split, the same
+partition yrtSetTileShard / yrtSetShardComm give the device) and gather_frame reassembles on
+rank 0 a frame bit-identical to the one-process render — the per-tile Random seeds
+(integratorrenderer.cpp:134) make the image partition-invariant."""
 import os
 import socket
 
@@ -29,29 +32,47 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _blob(W, H):
+    import yrt
+    from helpers import c2_args
+    d = yrt.Device(host=True)
+    s = yrt.Session(c2_args(W, 4) + ["-size", str(W), str(H), "-fb", "RGB_FLOAT32"], device=d)
+    b = s.export_frame()
+    s.close()
+    d.close()
+    return b
+
+
 def _worker(rank, world, port, W, H, q):
+    import oracle
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    rng = np.random.default_rng(7)
-    full = rng.random((H, W, 3), dtype=np.float32)
-    mine = np.where(tile_mask(W, H, rank, world)[..., None], full, 0).astype(np.float32)
+    img, st = oracle.render_shard(_blob(W, H), W, H, 1.0, rank, world, threads=2)
+    mine = np.where(tile_mask(W, H, rank, world)[..., None], img, 0).astype(np.float32)
+    assert not np.isnan(mine).any()
     t = torch.from_numpy(mine.copy())
     gather_frame(t, dst=0)
+    rays = torch.tensor([st["raysClosest"] + st["raysShadow"]], dtype=torch.float64)
+    dist.all_reduce(rays)
     if rank == 0:
-        q.put(bool(np.array_equal(t.numpy(), full)))
+        q.put((t.numpy(), float(rays.item())))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_gather_frame_world2():
-    W, H = 96, 80
+@pytest.mark.parametrize("world", [2])
+def test_gloo_tile_shards_render_and_gather(world):
+    import oracle
+    W, H = 88, 72
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, q)) for r in range(world)]
     for p in procs:
         p.start()
-    ok = q.get(timeout=120)
+    frame, rays = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
-    assert ok
     assert all(p.exitcode == 0 for p in procs)
+    full, st = oracle.render(_blob(W, H), W, H, 1.0)
+    assert np.array_equal(frame, full)
+    assert rays == st["raysClosest"] + st["raysShadow"]

@@ -328,3 +328,51 @@ def test_pick(gpu_device):
     hit, p = gpu_device.rtPick(cam, 0.5, 0.0, i["scene"])
     assert hit and abs(p[1] - 548.8) < 1.0
     s.close()
+
+
+# ----------------------------------------------------------------------------- multi-GPU (C++)
+@pytest.mark.parametrize("replica", [False, True])
+def test_multi_device_shards_bit_exact(gpu_device, monkeypatch, replica):
+    """yrtNewDevice("devices=0,0,0"): the frame's tiles dealt over three logical shards (one
+    host thread and one set of streams each), packed into slabs and gathered on the first
+    (SURVEY §8(e)); identical to the one-device frame, RGB_FLOAT32 and RGB8, progressive too.
+    replica: the scene is peer-copied to every shard (the multi-GPU replication path)."""
+    if replica:
+        monkeypatch.setenv("YRT_FORCE_SCENE_REPLICA", "1")
+    multi = yrt.Device(devices=[0, 0, 0])
+    assert multi.device_count() == 3
+    try:
+        for args in (c2_args(200, 4) + ["-fb", "RGB_FLOAT32"], c4_args(96, 2) + ["-fb", "RGB8"]):
+            face = 3 if "-stereo" in args else -1
+            imgs = []
+            for d in (gpu_device, multi):
+                s = yrt.Session(args, device=d)
+                a = s.render(face)
+                i = s.info()
+                d.rtRenderFrame(i["renderer"], s.camera(face), i["scene"], i["tonemapper"], i["framebuffer"], 1)
+                fmt = "RGB_FLOAT32" if "RGB_FLOAT32" in args else "RGB8"
+                b = d.framebuffer_array(i["framebuffer"], i["width"], i["height"], fmt)
+                imgs.append((a, b, d.render_stats()["raysClosest"]))
+                s.close()
+            assert np.array_equal(imgs[0][0], imgs[1][0])
+            assert np.array_equal(imgs[0][1], imgs[1][1])
+            assert imgs[0][2] == imgs[1][2]
+    finally:
+        multi.close()
+
+
+def test_startrt_multi_device_equals_single(tmp_path, monkeypatch):
+    """StartRT over YRT_DEVICES=0,0 (two logical shards of the GPU) writes the same strips as
+    over one device."""
+    from dae_scene import write
+    outs = []
+    for k, devs in enumerate(("0", "0,0")):
+        monkeypatch.setenv("YRT_DEVICES", devs)
+        d = tmp_path / f"r{k}"
+        f = write(d)
+        p = yrt.InitParamsRT()
+        p.size, p.spp, p.depth = 32, 2, 3
+        assert yrt.StartRT(f, p) and yrt.WaitRT()
+        assert yrt.GetLastErrorRT() == 0
+        outs.append([(d / f"room_{n}.jpg").read_bytes() for n in ("Kitchen", "Hall")])
+    assert outs[0] == outs[1]

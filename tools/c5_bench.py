@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""BASELINE config C5: the 22 Frederick St. interior stand-in (yrt.frederick, seed 2217) as a
+stereo FPR cubemap at the DLL's defaults with spp 1024 (YulioRT.h:37-50: 1536^2 faces, depth 10,
+tMaxShadowRay 120 x sceneScale, ambient .83 .95 .98, toe-in), on every GPU YRT_DEVICES names
+(default: all visible), through the product path.
+
+  (a) render-only: the FPR loop of one view through a Session (faceCamera update, scene refit,
+      rtRenderFrame per face, renderer.cpp:543-737) -> Mrays/s (closest + shadow queries,
+      pathtraceintegrator.cpp:74,161) and samples/s, timed face by face;
+  (b) end to end: StartRT -> WaitRT for both views (Collada load, BVH build, 24 faces, strip
+      assembly, JPEG) -> wall seconds;
+  (c) CPU baseline: the oracle on a band of face 0 at 16 spp (spp 16, scaled) on
+      every CPU this process may use, scaled linearly to the full 12-face 1024-spp cubemap.
+
+usage: python tools/c5_bench.py [--spp 1024] [--size 1536] [--views 1] [--no-startrt] [--cpu-rows 96]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "yulio-raytracer_amd"), str(ROOT)]
+
+import numpy as np  # noqa: E402
+
+import yrt  # noqa: E402
+from yrt import frederick  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--size", type=int, default=1536)
+    ap.add_argument("--views", type=int, default=1, help="FPR views timed render-only (a)")
+    ap.add_argument("--no-startrt", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=96)
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "c5_bench.json"))
+    a = ap.parse_args()
+    devs = os.environ.get("YRT_DEVICES", "all")
+    dae = frederick.write_dae(ROOT / "scenes" / "_generated" / "frederick_c5" / "frederick.dae")
+    res = {"config": {"workload": f"C5 frederick_standin (seed 2217) FPR stereo cubemap 12x{a.size}^2 {a.spp}spp "
+                                  "depth10 DLL defaults", "triangles": frederick.triangle_count(), "devices": devs}}
+
+    # (a) render only, face by face
+    dev = yrt.Device(devices=devs)
+    def args(spp):
+        return ["-fprCollada", "-faceCullingMode", "default", "-i", str(dae), "-stereo", "-size", str(a.size),
+                str(a.size), "-spp", str(spp), "-depth", "10", "-tMaxShadowRay", "120", "-ambientlight", "0.83",
+                "0.95", "0.98", "-toeIn"]
+    s = yrt.Session(args(a.spp), device=dev)
+    s.render_scene_camera(0)  # untimed: allocations, sample table
+    faces, rays, t_faces = [], 0.0, 0.0
+    for v in range(a.views):
+        for f in range(12):
+            t0 = time.perf_counter()
+            img = s.render_scene_camera(12 * v + f)
+            dt = time.perf_counter() - t0
+            st = dev.render_stats()
+            rays += st["raysClosest"] + st["raysShadow"]
+            t_faces += dt
+            faces.append({"face": 12 * v + f, "ms": round(dt * 1e3, 1), "mean_rgb8": round(float(img.mean()), 2),
+                          "rays_per_sample": round((st["raysClosest"] + st["raysShadow"]) / st["samples"], 3)})
+            print(f"face {12 * v + f}: {dt * 1e3:.0f} ms", flush=True)
+    samples = 12.0 * a.views * a.size * a.size * a.spp
+    res["render"] = {"devices": dev.device_count(), "views": a.views, "seconds": round(t_faces, 3),
+                     "ms_per_cubemap": round(t_faces / a.views * 1e3, 1), "Mrays_per_s": round(rays / t_faces / 1e6, 2),
+                     "Msamples_per_s": round(samples / t_faces / 1e6, 2), "rays": rays, "faces": faces}
+    s.close()
+    dev.close()
+
+    # (b) StartRT end to end (both views)
+    if not a.no_startrt:
+        p = yrt.InitParamsRT()
+        p.size, p.spp = a.size, a.spp
+        t0 = time.perf_counter()
+        assert yrt.StartRT(dae, p)
+        assert yrt.WaitRT()
+        dt = time.perf_counter() - t0
+        err = yrt.GetLastErrorRT()
+        outs = sorted(str(x.name) for x in dae.parent.glob("frederick_*.jpg"))
+        res["startrt"] = {"seconds": round(dt, 2), "views": len(frederick.CAMERAS), "error": err, "outputs": outs}
+        print(f"StartRT: {dt:.1f} s, error {err}, {outs}", flush=True)
+
+    # (c) CPU baseline on a band of face 0 at 16 spp, scaled
+    import oracle
+    cpu_spp = 16
+    hd = yrt.Device(host=True)
+    s_cpu = yrt.Session(args(cpu_spp), device=hd)
+    blob = s_cpu.export_frame(camera=s_cpu.scene_camera(0))
+    y0 = (a.size - a.cpu_rows) // 2
+    threads = oracle.cpu_count()
+    t0 = time.perf_counter()
+    _, st = oracle.render(blob, a.size, a.size, 1.0, rect=(0, y0, a.size, y0 + a.cpu_rows), threads=threads)
+    dt = time.perf_counter() - t0
+    cpu_rays = st["raysClosest"] + st["raysShadow"]
+    scale = (12.0 * a.size * a.size * a.spp) / (a.cpu_rows * a.size * cpu_spp)
+    res["cpu_baseline"] = {"kind": "port", "cores": threads, "sample": f"face 0 rows [{y0},{y0 + a.cpu_rows}) x "
+                           f"{a.size} px at {cpu_spp} spp ({cpu_rays:.0f} rays in {dt:.1f} s)",
+                           "Mrays_per_s": round(cpu_rays / dt / 1e6, 3),
+                           "Msamples_per_s": round(st["samples"] / dt / 1e6, 4),
+                           "scaled_seconds_per_cubemap": round(dt * scale, 1), "scale": round(scale, 1)}
+    s_cpu.close()
+    hd.close()
+    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
+    print(json.dumps({k: v for k, v in res.items() if k != "render"}, indent=1))
+    print(json.dumps({k: v for k, v in res["render"].items() if k != "faces"}))
+
+
+if __name__ == "__main__":
+    main()

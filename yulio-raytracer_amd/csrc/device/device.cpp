@@ -17,11 +17,13 @@
 #include <string>
 #include <memory>
 #include <deque>
+#include <thread>
 
 #include "../kernels/yrt_kernels.h"
 #include "image_io.h"
 #include "objects.h"
 #include "scene_gpu.h"
+#include "rccl_comm.h"
 #include "sampler.h"
 
 namespace yrt {
@@ -36,56 +38,16 @@ struct FrameCache {
   DevBuf dims, light;
 };
 
-class Device {
- public:
-  std::recursive_mutex mu;
-  std::string lastError;
-  std::set<HandleRef*> handles;
+// One HIP device's rendering state: its streams (lanes), the frame buffers, the wavefront
+// queues and the sample tables uploaded to it. A Device renders on one or several of these
+// (yrtNewDevice "devices=..."): 16x16 tiles are dealt round-robin over them,
+// one host thread drives each, and the frame is gathered on the first (rccl_comm.h).
+struct GpuCtx {
   int hipDevice = 0;
-  hipStream_t stream = nullptr;
-  uint32_t frameSeed = 0x2545F491u;
-  int64_t capacity = 64ll << 20;  // paths per batch: C3 +4 % over 16 M (fewer launch tails), ~10 GB
-  int shardIndex = 0, shardCount = 1;
-  bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
-  bool kernelTiming = false;
-  YRTRenderStats stats{};
-  // ray capture (roofline accounting): strided sample of each depth's query streams, batch 0
-  int captureMax = 0;
-  struct Captured { std::vector<float> org, dir; double total = 0; };
-  std::vector<Captured> capClosest, capShadow;
-  // counts: the queue's first segment counter; segments of segCap slots
-  void capture(std::vector<Captured>& out, int depth, const float4* org, const float4* dir, const unsigned* counts,
-               int segCap, hipStream_t stream) {
-    std::vector<unsigned> cs((size_t)YRT_QSEGS * YRT_QCSTRIDE);
-    HIP_CHECK(hipMemcpyAsync(cs.data(), counts, cs.size() * sizeof(unsigned), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
-    size_t n = 0;
-    for (int k = 0; k < YRT_QSEGS; ++k) n += cs[(size_t)k * YRT_QCSTRIDE];
-    if ((int)out.size() <= depth) out.resize(depth + 1);
-    Captured& c = out[depth];
-    c.total = (double)n;
-    c.org.clear();
-    c.dir.clear();
-    const size_t stride = std::max<size_t>(1, (n + captureMax - 1) / captureMax);
-    for (int k = 0; k < YRT_QSEGS; ++k) {
-      const size_t nk = cs[(size_t)k * YRT_QCSTRIDE];
-      const size_t m = nk ? (nk + stride - 1) / stride : 0;
-      if (!m) continue;
-      const size_t at = c.org.size();
-      c.org.resize(at + m * 4);
-      c.dir.resize(at + m * 4);
-      HIP_CHECK(hipMemcpy2D(c.org.data() + at, 16, org + (size_t)k * segCap, stride * 16, 16, m,
-                            hipMemcpyDeviceToHost));
-      HIP_CHECK(hipMemcpy2D(c.dir.data() + at, 16, dir + (size_t)k * segCap, stride * 16, 16, m,
-                            hipMemcpyDeviceToHost));
-    }
-  }
-
-  // per-frame device state
-  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount;
+  hipStream_t stream = nullptr;  // lanes[0].stream
   // A wavefront lane: a stream and the batch state it owns. Batches alternate between the
   // lanes so one batch's kernels run beside the other's (the VALU-bound traversal next to the
-  // latency-bound shading); lane 0's stream is also the device's stream for everything else.
+  // latency-bound shading).
   struct Lane {
     hipStream_t stream = nullptr;
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
@@ -98,50 +60,41 @@ class Device {
   static constexpr int kMaxLanes = 2;
   Lane lanes[kMaxLanes];
   int numLanes = kMaxLanes;
+  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab;
+  std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
   static constexpr size_t kMaxFrameCaches = 16;
   std::map<std::string, std::unique_ptr<FrameCache>> fcaches;
   std::deque<std::string> fcacheOrder;
   std::vector<hipEvent_t> eventPool;
+  YRTRenderStats stats{};
+  struct Captured { std::vector<float> org, dir; double total = 0; };
+  std::vector<Captured> capClosest, capShadow;
 
-  bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
-  explicit Device(int dev, bool useGpu) : hipDevice(dev), gpu(useGpu) {
-    if (!gpu) return;
+  GpuCtx(int dev, int lanesWanted) : hipDevice(dev), numLanes(lanesWanted) {
     HIP_CHECK(hipSetDevice(hipDevice));
     for (Lane& L : lanes) HIP_CHECK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
     stream = lanes[0].stream;
-    if (const char* e = getenv("YRT_LANES")) numLanes = std::max(1, std::min(kMaxLanes, atoi(e)));
   }
-  ~Device() {
-    for (auto* h : handles) delete h;
+  ~GpuCtx() {
+    (void)hipSetDevice(hipDevice);
     for (auto e : eventPool) (void)hipEventDestroy(e);
     for (Lane& L : lanes) {
       if (L.hc) (void)hipHostFree(L.hc);
       if (L.stream) (void)hipStreamDestroy(L.stream);
     }
   }
-
-  YRTHandle wrap(std::shared_ptr<Object> o) {
-    o->dev = this;
-    auto* h = new HandleRef();
-    h->obj = std::move(o);
-    handles.insert(h);
-    return (YRTHandle)h;
+  hipEvent_t ev() {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    eventPool.push_back(e);
+    return e;
   }
-  HandleRef* ref(YRTHandle h) {
-    auto* r = (HandleRef*)h;
-    if (!r || handles.find(r) == handles.end()) throw std::runtime_error("invalid handle");
-    return r;
+  int* spill() {
+    dSpill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
+    return dSpill.as<int>();
   }
-  template <class T>
-  std::shared_ptr<T> get(YRTHandle h, const char* what) {
-    if (!h) return nullptr;
-    auto o = std::dynamic_pointer_cast<T>(ref(h)->obj);
-    if (!o) throw std::runtime_error(std::string("invalid ") + what + " handle");
-    return o;
-  }
-
   // P paths per batch; queues hold YRT_QSEGS segments of qseg_capacity(P) slots
   static void ensure_paths(Lane& L, int64_t P, int numLights) {
     const int64_t Q = (int64_t)YRT_QSEGS * qseg_capacity(P);
@@ -166,21 +119,121 @@ class Device {
       L.shadowCap = S;
     }
   }
+  // ray capture (roofline accounting): strided sample of each depth's query streams, batch 0
+  // counts: the queue's first segment counter; segments of segCap slots
+  void capture(int captureMax, std::vector<Captured>& out, int depth, const float4* org, const float4* dir,
+               const unsigned* counts, int segCap, hipStream_t st) {
+    std::vector<unsigned> cs((size_t)YRT_QSEGS * YRT_QCSTRIDE);
+    HIP_CHECK(hipMemcpyAsync(cs.data(), counts, cs.size() * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    size_t n = 0;
+    for (int k = 0; k < YRT_QSEGS; ++k) n += cs[(size_t)k * YRT_QCSTRIDE];
+    if ((int)out.size() <= depth) out.resize(depth + 1);
+    Captured& c = out[depth];
+    c.total = (double)n;
+    c.org.clear();
+    c.dir.clear();
+    const size_t stride = std::max<size_t>(1, (n + captureMax - 1) / captureMax);
+    for (int k = 0; k < YRT_QSEGS; ++k) {
+      const size_t nk = cs[(size_t)k * YRT_QCSTRIDE];
+      const size_t m = nk ? (nk + stride - 1) / stride : 0;
+      if (!m) continue;
+      const size_t at = c.org.size();
+      c.org.resize(at + m * 4);
+      c.dir.resize(at + m * 4);
+      HIP_CHECK(hipMemcpy2D(c.org.data() + at, 16, org + (size_t)k * segCap, stride * 16, 16, m,
+                            hipMemcpyDeviceToHost));
+      HIP_CHECK(hipMemcpy2D(c.dir.data() + at, 16, dir + (size_t)k * segCap, stride * 16, 16, m,
+                            hipMemcpyDeviceToHost));
+    }
+  }
+};
 
-  DevBuf dSpill;  // deep traversal-stack entries of k_trace (rarely touched)
-  int* spill() {
-    dSpill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
-    return dSpill.as<int>();
+// the tiles of shard (index, count): tile = index + j * count, j < shard_tiles
+static int shard_tiles(int numTiles, int index, int count) {
+  return numTiles > index ? (numTiles - index + count - 1) / count : 0;
+}
+
+class Device {
+ public:
+  std::recursive_mutex mu;
+  std::string lastError;
+  std::set<HandleRef*> handles;
+  std::vector<std::unique_ptr<GpuCtx>> ctx;  // ctx[0]: the primary device (commits, queries, output)
+  int hipDevice = 0;                         // ctx[0]'s
+  hipStream_t stream = nullptr;              // ctx[0]'s
+  uint32_t frameSeed = 0x2545F491u;
+  int64_t capacity = 64ll << 20;  // paths per batch: C3 +4 % over 16 M (fewer launch tails), ~10 GB
+  // process-level shard (yrtSetTileShard / yrtSetShardComm): this process renders tiles
+  // t = shardIndex (mod shardCount), dealt over its own devices
+  int shardIndex = 0, shardCount = 1;
+  ncclComm_t procComm = nullptr;     // process-level gather to rank 0 (yrtSetShardComm)
+  ncclComm_t localComm = nullptr;    // the ctx devices' gather (distinct devices only): rank 0's
+  std::vector<ncclComm_t> localComms;  // one per ctx device (ncclCommInitAll)
+  bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
+  bool kernelTiming = false;
+  YRTRenderStats stats{};
+  int captureMax = 0;
+
+  bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
+  Device(const std::vector<int>& devs, bool useGpu) : gpu(useGpu) {
+    if (!gpu) return;
+    int lanes = GpuCtx::kMaxLanes;
+    if (const char* e = getenv("YRT_LANES")) lanes = std::max(1, std::min(GpuCtx::kMaxLanes, atoi(e)));
+    for (int d : devs) ctx.emplace_back(new GpuCtx(d, lanes));
+    hipDevice = ctx[0]->hipDevice;
+    stream = ctx[0]->stream;
+    HIP_CHECK(hipSetDevice(hipDevice));
+  }
+  ~Device() {
+    for (auto* h : handles) delete h;
+    handles.clear();
+    try {
+      for (auto c : localComms) rccl().CommDestroy(c);
+      if (procComm) rccl().CommDestroy(procComm);
+    } catch (...) {
+    }
   }
 
-  hipEvent_t ev() {
-    hipEvent_t e;
-    HIP_CHECK(hipEventCreate(&e));
-    eventPool.push_back(e);
-    return e;
+  YRTHandle wrap(std::shared_ptr<Object> o) {
+    o->dev = this;
+    auto* h = new HandleRef();
+    h->obj = std::move(o);
+    handles.insert(h);
+    return (YRTHandle)h;
+  }
+  HandleRef* ref(YRTHandle h) {
+    auto* r = (HandleRef*)h;
+    if (!r || handles.find(r) == handles.end()) throw std::runtime_error("invalid handle");
+    return r;
+  }
+  template <class T>
+  std::shared_ptr<T> get(YRTHandle h, const char* what) {
+    if (!h) return nullptr;
+    auto o = std::dynamic_pointer_cast<T>(ref(h)->obj);
+    if (!o) throw std::runtime_error(std::string("invalid ") + what + " handle");
+    return o;
+  }
+
+  int* spill() { return ctx[0]->spill(); }
+
+  // the committed scene as seen by one of the devices (a peer copy, refreshed after rebuilds
+  // and refits; logical shards on the primary's own device share its buffers)
+  // YRT_FORCE_SCENE_REPLICA=1 (tests): peer-copy the scene even onto the primary's own device,
+  // so a one-GPU box exercises the replication path of multi-GPU renders
+  GpuScene& scene_on(SceneObj& S, int dev, bool primary) {
+    static const bool force = getenv("YRT_FORCE_SCENE_REPLICA") != nullptr;
+    if (dev == S.gpu->device && (primary || !force)) return *S.gpu;
+    auto& r = S.replicas[dev];
+    if (!r || r->serial != S.gpu->serial || r->refits != S.gpu->refits) r = replicate_gpu_scene(*S.gpu, dev);
+    return *r;
   }
 
   void render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F, int accumulate);
+  void render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, ToneMapperObj& T, int W, int H,
+                    int index, int count, int accumulate, bool reportProgress);
+  void gather_local(int W, int H, int numTiles);
+  void gather_process(int W, int H, int numTiles);
   void intersect(SceneObj& S, const float* org4, const float* dir4, uint32_t n, float* hit4, int32_t* occ,
                  hipStream_t st);
 };
@@ -193,14 +246,89 @@ static void status(RendererObj& R, int state, float progress) {
 void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F,
                     int accumulate) {
   auto t0 = std::chrono::steady_clock::now();
-  HIP_CHECK(hipSetDevice(hipDevice));
   if (!S.gpu) throw std::runtime_error("scene not committed");
   if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
-  GpuScene& G = *S.gpu;
-  SceneView sv = G.view;
-  sv.traceSpill = spill();
   const int W = F.width, H = F.height;
+  const int numTiles = ((W + 15) / 16) * ((H + 15) / 16);
   memset(&stats, 0, sizeof(stats));
+  if (!accumulate) R.iteration = 0;
+  const int N = (int)ctx.size();
+  // the debug renderer is a one-pass traversal KAT: the primary device renders every tile
+  const int nr = R.debug ? 1 : N;
+  std::vector<GpuScene*> scenes(nr);
+  for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
+  if (nr == 1) {
+    render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
+  } else {
+    // device k of this process renders the tiles t = shardIndex + k * shardCount (mod shardCount * N)
+    std::vector<std::string> errs(nr);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nr; ++k)
+      th.emplace_back([&, k] {
+        try {
+          render_shard(*ctx[k], *scenes[k], R, C, T, W, H, shardIndex + k * shardCount, shardCount * nr, accumulate,
+                       k == 0);
+        } catch (const std::exception& e) {
+          errs[k] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw std::runtime_error(e);
+    gather_local(W, H, numTiles);
+  }
+  R.iteration++;
+  for (int k = 0; k < nr; ++k) {
+    const YRTRenderStats& s = ctx[k]->stats;
+    stats.raysClosest += s.raysClosest;
+    stats.raysShadow += s.raysShadow;
+    stats.launchesClosest += s.launchesClosest;
+    stats.launchesShadow += s.launchesShadow;
+    stats.msTraceClosest = std::max(stats.msTraceClosest, s.msTraceClosest);
+    stats.msTraceShadow = std::max(stats.msTraceShadow, s.msTraceShadow);
+    stats.msShade = std::max(stats.msShade, s.msShade);
+  }
+  if (!R.debug && shardCount > 1 && procComm) gather_process(W, H, numTiles);
+
+  // framebuffer write-back (api/framebuffer.h:93-226) from the primary device
+  GpuCtx& g0 = *ctx[0];
+  HIP_CHECK(hipSetDevice(g0.hipDevice));
+  const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
+  void* dst = F.buffer(F.cur);
+  if (F.format == FB_RGB8) {
+    HIP_CHECK(hipMemcpy(dst, g0.dFbRGB8.p, rgb8Stride * H, hipMemcpyDeviceToHost));
+  } else {
+    std::vector<float> tmp((size_t)W * H * 3);
+    HIP_CHECK(hipMemcpy(tmp.data(), g0.dFbFloat.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+    if (F.format == FB_RGB_FLOAT32) {
+      memcpy(dst, tmp.data(), tmp.size() * sizeof(float));
+    } else if (F.format == FB_RGBA_FLOAT32) {
+      float* o = (float*)dst;
+      for (size_t i = 0; i < (size_t)W * H; ++i) {
+        o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
+      }
+    } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
+      uint8_t* o = (uint8_t*)dst;
+      for (size_t i = 0; i < (size_t)W * H; ++i) {
+        for (int k = 0; k < 3; ++k) o[4 * i + k] = (uint8_t)clampf(tmp[3 * i + k] * 255.0f, 0.0f, 255.0f);
+        o[4 * i + 3] = 0;
+      }
+    }
+  }
+  stats.samples = ctx[0]->stats.samples;
+  stats.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  status(R, 2, 1.f);
+}
+
+// Renders the tiles of shard (index, count) of the frame into g's full-size buffers (the other
+// tiles' pixels are left zero when count > 1).
+void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, ToneMapperObj& T, int W, int H,
+                          int index, int count, int accumulate, bool reportProgress) {
+  HIP_CHECK(hipSetDevice(g.hipDevice));
+  memset(&g.stats, 0, sizeof(g.stats));
+  SceneView sv = G.view;
+  sv.traceSpill = g.spill();
+  const hipStream_t stream = g.stream;
 
   GpuRenderParams rp;
   memset(&rp, 0, sizeof(rp));
@@ -225,7 +353,6 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
   rp.numPrecomp = (int)G.precomputed.size();
 
   // samples: PathTraceIntegrator::requestSamples (pathtraceintegrator.cpp:35-47)
-  if (!accumulate) R.iteration = 0;
   SampleRequest req;
   req.spp = R.debug ? 1 : R.spp;
   req.sets = R.sets;
@@ -242,79 +369,77 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
   char keybuf[256];
   snprintf(keybuf, sizeof(keybuf), "%d/%d/%d/%d/%d/%s/%llu", req.spp, req.sets, req.iteration, req.num1D, req.num2D,
            req.filter.c_str(), (unsigned long long)G.serial);
-  auto fit = fcaches.find(keybuf);
-  if (fit == fcaches.end()) {
-    if (fcaches.size() >= kMaxFrameCaches) {
-      fcaches.erase(fcacheOrder.front());
-      fcacheOrder.pop_front();
+  auto fit = g.fcaches.find(keybuf);
+  if (fit == g.fcaches.end()) {
+    if (g.fcaches.size() >= GpuCtx::kMaxFrameCaches) {
+      g.fcaches.erase(g.fcacheOrder.front());
+      g.fcacheOrder.pop_front();
     }
     auto fc = std::make_unique<FrameCache>();
     build_sample_table(req, fc->table);
     fc->dims.upload(fc->table.dims);
     fc->light.upload(fc->table.light);
     fc->key = keybuf;
-    fcacheOrder.push_back(keybuf);
-    fit = fcaches.emplace(keybuf, std::move(fc)).first;
+    g.fcacheOrder.push_back(keybuf);
+    fit = g.fcaches.emplace(keybuf, std::move(fc)).first;
   }
   FrameCache& fcache = *fit->second;
   const SampleTable& tab = fcache.table;
   rp.spp = tab.spp;
   rp.sets = tab.sets;
 
-  dRp.alloc(sizeof(rp));
-  dCam.alloc(sizeof(GpuCamera));
-  HIP_CHECK(hipMemcpyAsync(dRp.p, &rp, sizeof(rp), hipMemcpyHostToDevice, stream));
-  HIP_CHECK(hipMemcpyAsync(dCam.p, &C.cam, sizeof(GpuCamera), hipMemcpyHostToDevice, stream));
-  dPixelSets.alloc((size_t)W * H);
+  g.dRp.alloc(sizeof(rp));
+  g.dCam.alloc(sizeof(GpuCamera));
+  HIP_CHECK(hipMemcpyAsync(g.dRp.p, &rp, sizeof(rp), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(g.dCam.p, &C.cam, sizeof(GpuCamera), hipMemcpyHostToDevice, stream));
+  g.dPixelSets.alloc((size_t)W * H);
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  dFbFloat.alloc((size_t)W * H * 3 * sizeof(float));
-  dFbRGB8.alloc(rgb8Stride * H);
-  if (shardCount > 1) {  // pixels of other shards stay 0 so per-rank images compose by sum
-    HIP_CHECK(hipMemsetAsync(dFbFloat.p, 0, (size_t)W * H * 3 * sizeof(float), stream));
-    HIP_CHECK(hipMemsetAsync(dFbRGB8.p, 0, rgb8Stride * H, stream));
+  g.dFbFloat.alloc((size_t)W * H * 3 * sizeof(float));
+  g.dFbRGB8.alloc(rgb8Stride * H);
+  if (count > 1) {  // pixels of other shards stay 0 so per-shard images compose by sum
+    HIP_CHECK(hipMemsetAsync(g.dFbFloat.p, 0, (size_t)W * H * 3 * sizeof(float), stream));
+    HIP_CHECK(hipMemsetAsync(g.dFbRGB8.p, 0, rgb8Stride * H, stream));
   }
 
   FrameView fv;
-  fv.rp = dRp.as<GpuRenderParams>();
-  fv.cam = dCam.as<GpuCamera>();
+  fv.rp = g.dRp.as<GpuRenderParams>();
+  fv.cam = g.dCam.as<GpuCamera>();
   fv.samples = fcache.dims.as<float>();
   fv.lightSamples = fcache.light.as<float>();
-  fv.pixelSets = dPixelSets.as<uint8_t>();
+  fv.pixelSets = g.dPixelSets.as<uint8_t>();
   fv.numRecords = tab.numRecords;
   fv.numLightSlots = std::max(1, tab.numLightSlots);
 
-  status(R, 1, 0.f);
+  if (reportProgress) status(R, 1, 0.f);
   const int numTiles = rp.numTilesX * rp.numTilesY;
-  // tiles of this shard: tile = shardIndex + k * shardCount
-  const int shardTiles = numTiles > shardIndex ? (numTiles - shardIndex + shardCount - 1) / shardCount : 0;
+  const int shardTiles = shard_tiles(numTiles, index, count);
 
   if (R.debug) {
-    launch_debug_render(G.view, fv, R.maxDepth, R.spp, numTiles, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(),
+    launch_debug_render(sv, fv, R.maxDepth, R.spp, numTiles, g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(),
                         (int)rgb8Stride, stream);
-    stats.raysClosest = 0;
   } else {
-    launch_pixel_sets(fv, dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
-    capClosest.clear();
-    capShadow.clear();
+    launch_pixel_sets(fv, g.dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
+    g.capClosest.clear();
+    g.capShadow.clear();
     const int spp = rp.spp;
     int64_t tilesPerBatch = std::max<int64_t>(1, capacity / (256ll * spp));
     // a multiple of the lanes in batches (evenly sized), so both lanes have work even when a
     // shard of the frame fits one batch (multi-GPU shards, small frames)
-    if (captureMax == 0 && numLanes > 1 && shardTiles > 1) {
+    if (captureMax == 0 && g.numLanes > 1 && shardTiles > 1) {
       int64_t nb = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
-      nb = (nb + numLanes - 1) / numLanes * numLanes;
+      nb = (nb + g.numLanes - 1) / g.numLanes * g.numLanes;
       tilesPerBatch = (shardTiles + nb - 1) / nb;
     }
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
     const int64_t numBatches = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
-    const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(numLanes, numBatches));
+    const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
     const size_t counterWords = qcounter_index(levels, 0, 0);
-    dAccu.alloc((size_t)W * H * 16);
+    g.dAccu.alloc((size_t)W * H * 16);
     for (int l = 0; l < nl; ++l) {
-      Lane& L = lanes[l];
-      ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights);
+      GpuCtx::Lane& L = g.lanes[l];
+      GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights);
       L.counters.alloc(counterWords * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
       if (L.hcWords < counterWords) {
@@ -326,11 +451,11 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     }
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
     if (nl > 1) {
-      hipEvent_t setup = ev();
+      hipEvent_t setup = g.ev();
       HIP_CHECK(hipEventRecord(setup, stream));
-      for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(lanes[l].stream, setup, 0));
+      for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(g.lanes[l].stream, setup, 0));
     }
-    auto lane_buffers = [&](Lane& L) {
+    auto lane_buffers = [&](GpuCtx::Lane& L) {
       PathBuffers pb;
       for (int k = 0; k < 2; ++k) {
         pb.qPath[k] = L.qPath[k].as<int>();
@@ -360,7 +485,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + 65536; };
     // waits for the lane's previous batch and accounts its queue counters
     int64_t tilesDone = 0;
-    auto drain = [&](Lane& L) {
+    auto drain = [&](GpuCtx::Lane& L) {
       if (!L.pending) return;
       HIP_CHECK(hipStreamSynchronize(L.stream));
       for (int d = 0; d < levels; ++d) {
@@ -372,15 +497,15 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
         estClosest[d] = (long long)nc;
         estShadow[d] = (long long)ns;
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
-          stats.raysClosest += nc;
-          if (nc) stats.launchesClosest += 1;
+          g.stats.raysClosest += nc;
+          if (nc) g.stats.launchesClosest += 1;
         }
-        stats.raysShadow += ns;
-        if (d < rp.maxDepth && ns) stats.launchesShadow += 1;
+        g.stats.raysShadow += ns;
+        if (d < rp.maxDepth && ns) g.stats.launchesShadow += 1;
       }
       L.pending = false;
       tilesDone += L.pendTiles;
-      status(R, 1, float(tilesDone) / float(std::max(1, shardTiles)));
+      if (reportProgress) status(R, 1, float(tilesDone) / float(std::max(1, shardTiles)));
     };
 
     struct EvPair { hipEvent_t a, b; int kind; };
@@ -388,7 +513,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     int64_t batch = 0;
     for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
       if (R.stopFlag && R.stopFlag->load()) break;
-      Lane& L = lanes[batch % nl];
+      GpuCtx::Lane& L = g.lanes[batch % nl];
       drain(L);
       const hipStream_t st = L.stream;
       const PathBuffers pb = lane_buffers(L);
@@ -397,80 +522,150 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
       BatchInfo bi;
       bi.firstTile = (int)first;
       bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
-      bi.tileStride = shardCount;
-      bi.tileOffset = shardIndex;
+      bi.tileStride = count;
+      bi.tileOffset = index;
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
       launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
         EvPair e1{};
-        if (kernelTiming) { e1 = {ev(), ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
+        if (kernelTiming) { e1 = {g.ev(), g.ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
         launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
                              pb.segCap, pb.hit, st, hint(estClosest[d]));
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
-          capture(capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), pb.segCap, st);
+          g.capture(captureMax, g.capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0),
+                    pb.segCap, st);
         EvPair e2{};
-        if (kernelTiming) { e2 = {ev(), ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
+        if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
         launch_shade(lsv, fv, pb, bi, d, G.materialMask, st, hint(estClosest[d]));
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (rp.numLights > 0) {
           EvPair e3{};
-          if (kernelTiming) { e3 = {ev(), ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
+          if (kernelTiming) { e3 = {g.ev(), g.ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
           const ShadowFuse sf{pb.sContrib, pb.pathL};
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
                            pb.sOcc, st, pb.fuseShadow ? &sf : nullptr, hint(estShadow[d]));
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
-            capture(capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), pb.shSegCap, st);
+            g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),
+                      pb.shSegCap, st);
           if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, st, hint(estClosest[d]));
         }
       }
-      launch_resolve_pixels(fv, pb, bi, dFbFloat.as<float>(), dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
-                            dAccu.as<float4>(), accumulate ? 1 : 0, st);
+      launch_resolve_pixels(fv, pb, bi, g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
+                            g.dAccu.as<float4>(), accumulate ? 1 : 0, st);
       HIP_CHECK(hipMemcpyAsync(L.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       L.pending = true;
       L.pendTiles = bi.numPixels / 256;
     }
-    for (int l = 0; l < nl; ++l) drain(lanes[l]);
+    for (int l = 0; l < nl; ++l) drain(g.lanes[l]);
     for (auto& e : evs) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));
-      if (e.kind == 0) stats.msTraceClosest += ms;
-      else if (e.kind == 1) stats.msTraceShadow += ms;
-      else stats.msShade += ms;
+      if (e.kind == 0) g.stats.msTraceClosest += ms;
+      else if (e.kind == 1) g.stats.msTraceShadow += ms;
+      else g.stats.msShade += ms;
     }
-    for (auto e : eventPool) (void)hipEventDestroy(e);
-    eventPool.clear();
-    R.iteration++;
+    for (auto e : g.eventPool) (void)hipEventDestroy(e);
+    g.eventPool.clear();
   }
-  for (int l = 0; l < kMaxLanes; ++l) HIP_CHECK(hipStreamSynchronize(lanes[l].stream));
+  for (int l = 0; l < GpuCtx::kMaxLanes; ++l) HIP_CHECK(hipStreamSynchronize(g.lanes[l].stream));
+  g.stats.samples = (double)W * H * (R.debug ? 1 : rp.spp);
+}
 
-  // framebuffer write-back (api/framebuffer.h:93-226)
-  void* dst = F.buffer(F.cur);
-  if (F.format == FB_RGB8) {
-    HIP_CHECK(hipMemcpy(dst, dFbRGB8.p, rgb8Stride * H, hipMemcpyDeviceToHost));
+// The ctx devices' shards onto ctx[0]: every peer packs its tiles into a slab, the slabs go to
+// the first device (RCCL grouped send/recv when the devices are distinct GPUs — one xGMI link
+// per peer; a device-to-device copy when logical shards share a GPU) and are unpacked there.
+void Device::gather_local(int W, int H, int numTiles) {
+  const int N = (int)ctx.size();
+  const int rgb8Stride = (3 * W + 3) / 4 * 4;
+  bool distinct = true;
+  for (int a = 0; a < N; ++a)
+    for (int b = a + 1; b < N; ++b) distinct &= ctx[a]->hipDevice != ctx[b]->hipDevice;
+  GpuCtx& g0 = *ctx[0];
+  std::vector<int> tiles(N);
+  for (int k = 1; k < N; ++k) {
+    GpuCtx& g = *ctx[k];
+    tiles[k] = shard_tiles(numTiles, shardIndex + k * shardCount, shardCount * N);
+    HIP_CHECK(hipSetDevice(g.hipDevice));
+    g.dSlab.alloc((size_t)std::max(1, tiles[k]) * 256 * sizeof(float4));
+    launch_pack_tiles(g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), W, H, rgb8Stride, shardIndex + k * shardCount,
+                      shardCount * N, tiles[k], g.dSlab.as<float4>(), g.stream);
+    HIP_CHECK(hipSetDevice(g0.hipDevice));
+    g0.recvSlabs[k].alloc((size_t)std::max(1, tiles[k]) * 256 * sizeof(float4));
+  }
+  if (distinct) {
+    const RcclApi& nc = rccl();
+    if (!localComm) {
+      std::vector<int> devs;
+      for (auto& g : ctx) devs.push_back(g->hipDevice);
+      std::vector<ncclComm_t> comms(N);
+      rccl_check(nc.CommInitAll(comms.data(), N, devs.data()), "ncclCommInitAll");
+      localComms.assign(comms.begin(), comms.end());
+      localComm = comms[0];
+    }
+    rccl_check(nc.GroupStart(), "ncclGroupStart");
+    for (int k = 1; k < N; ++k) {
+      const size_t bytes = (size_t)tiles[k] * 256 * sizeof(float4);
+      if (!bytes) continue;
+      rccl_check(nc.Send(ctx[k]->dSlab.p, bytes, ncclUint8, 0, localComms[k], ctx[k]->stream), "ncclSend");
+      rccl_check(nc.Recv(g0.recvSlabs[k].p, bytes, ncclUint8, k, localComms[0], g0.stream), "ncclRecv");
+    }
+    rccl_check(nc.GroupEnd(), "ncclGroupEnd");
   } else {
-    std::vector<float> tmp((size_t)W * H * 3);
-    HIP_CHECK(hipMemcpy(tmp.data(), dFbFloat.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
-    if (F.format == FB_RGB_FLOAT32) {
-      memcpy(dst, tmp.data(), tmp.size() * sizeof(float));
-    } else if (F.format == FB_RGBA_FLOAT32) {
-      float* o = (float*)dst;
-      for (size_t i = 0; i < (size_t)W * H; ++i) {
-        o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
-      }
-    } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
-      uint8_t* o = (uint8_t*)dst;
-      for (size_t i = 0; i < (size_t)W * H; ++i) {
-        for (int k = 0; k < 3; ++k) o[4 * i + k] = (uint8_t)clampf(tmp[3 * i + k] * 255.0f, 0.0f, 255.0f);
-        o[4 * i + 3] = 0;
-      }
+    for (int k = 1; k < N; ++k) {
+      HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
+      const size_t bytes = (size_t)tiles[k] * 256 * sizeof(float4);
+      if (bytes)
+        HIP_CHECK(hipMemcpyPeerAsync(g0.recvSlabs[k].p, g0.hipDevice, ctx[k]->dSlab.p, ctx[k]->hipDevice, bytes,
+                                     g0.stream));
     }
   }
-  stats.samples = (double)W * H * rp.spp;
-  stats.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  status(R, 2, 1.f);
+  HIP_CHECK(hipSetDevice(g0.hipDevice));
+  for (int k = 1; k < N; ++k)
+    launch_unpack_tiles(g0.recvSlabs[k].as<float4>(), g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H,
+                        rgb8Stride, shardIndex + k * shardCount, shardCount * N, tiles[k], g0.stream);
+  for (int k = 0; k < N; ++k) {
+    HIP_CHECK(hipSetDevice(ctx[k]->hipDevice));
+    HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
+  }
+  HIP_CHECK(hipSetDevice(g0.hipDevice));
+}
+
+// This process's tiles (shard shardIndex of shardCount, already gathered on ctx[0]) to rank 0
+// of the process communicator (yrtSetShardComm): every rank packs its tiles, rank 0 receives
+// each peer's slab (grouped RCCL send/recv) and unpacks it into its frame.
+void Device::gather_process(int W, int H, int numTiles) {
+  const RcclApi& nc = rccl();
+  GpuCtx& g0 = *ctx[0];
+  HIP_CHECK(hipSetDevice(g0.hipDevice));
+  const int rgb8Stride = (3 * W + 3) / 4 * 4;
+  const int P = shardCount;
+  if (shardIndex != 0) {
+    const int tiles = shard_tiles(numTiles, shardIndex, P);
+    g0.dSlab.alloc((size_t)std::max(1, tiles) * 256 * sizeof(float4));
+    launch_pack_tiles(g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H, rgb8Stride, shardIndex, P, tiles,
+                      g0.dSlab.as<float4>(), g0.stream);
+    if (tiles) rccl_check(nc.Send(g0.dSlab.p, (size_t)tiles * 256 * sizeof(float4), ncclUint8, 0, procComm, g0.stream),
+                          "ncclSend");
+  } else {
+    std::vector<int> tiles(P);
+    for (int r = 1; r < P; ++r) {
+      tiles[r] = shard_tiles(numTiles, r, P);
+      g0.recvSlabs[r].alloc((size_t)std::max(1, tiles[r]) * 256 * sizeof(float4));
+    }
+    rccl_check(nc.GroupStart(), "ncclGroupStart");
+    for (int r = 1; r < P; ++r)
+      if (tiles[r])
+        rccl_check(nc.Recv(g0.recvSlabs[r].p, (size_t)tiles[r] * 256 * sizeof(float4), ncclUint8, r, procComm,
+                           g0.stream), "ncclRecv");
+    rccl_check(nc.GroupEnd(), "ncclGroupEnd");
+    for (int r = 1; r < P; ++r)
+      launch_unpack_tiles(g0.recvSlabs[r].as<float4>(), g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H,
+                          rgb8Stride, r, P, tiles[r], g0.stream);
+  }
+  HIP_CHECK(hipStreamSynchronize(g0.stream));
 }
 
 // ---------------------------------------------------------------- ray queries
@@ -478,14 +673,15 @@ void Device::intersect(SceneObj& S, const float* org4, const float* dir4, uint32
                        hipStream_t st) {
   HIP_CHECK(hipSetDevice(hipDevice));
   if (!S.gpu) throw std::runtime_error("scene not committed");
-  dCount.alloc(sizeof(unsigned));
-  HIP_CHECK(hipMemcpyAsync(dCount.p, &n, sizeof(unsigned), hipMemcpyHostToDevice, st));
+  GpuCtx& g = *ctx[0];
+  g.dCount.alloc(sizeof(unsigned));
+  HIP_CHECK(hipMemcpyAsync(g.dCount.p, &n, sizeof(unsigned), hipMemcpyHostToDevice, st));
   SceneView sv = S.gpu->view;
   sv.traceSpill = spill();
   if (occ)
-    launch_trace_any(sv, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n, occ, st);
+    launch_trace_any(sv, (const float4*)org4, (const float4*)dir4, g.dCount.as<unsigned>(), 1, (int)n, occ, st);
   else
-    launch_trace_closest(sv, (const float4*)org4, (const float4*)dir4, dCount.as<unsigned>(), 1, (int)n,
+    launch_trace_closest(sv, (const float4*)org4, (const float4*)dir4, g.dCount.as<unsigned>(), 1, (int)n,
                          (float4*)hit4, st);
   HIP_CHECK(hipStreamSynchronize(st));
 }
@@ -525,14 +721,32 @@ struct YRTDevice_ {
 
 extern "C" {
 
+// parms: "" or "device=<k>" (one HIP device), "devices=<a,b,...>" or "devices=all" (tiles dealt
+// over several; a device id may repeat: logical shards on one GPU), "host" (no GPU: loaders,
+// BVH and frame export only, for CPU tests)
 YRTDevice yrtNewDevice(const char* parms, size_t, int, const char*) {
-  int devId = 0;
+  std::vector<int> devs = {0};
   bool gpu = true;
-  if (parms && strncmp(parms, "device=", 7) == 0) devId = atoi(parms + 7);
-  if (parms && strcmp(parms, "host") == 0) gpu = false;
   try {
+    if (parms && strncmp(parms, "device=", 7) == 0) devs = {atoi(parms + 7)};
+    if (parms && strncmp(parms, "devices=", 8) == 0) {
+      devs.clear();
+      if (!strcmp(parms + 8, "all")) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return nullptr;
+        for (int k = 0; k < n; ++k) devs.push_back(k);
+      } else {
+        for (const char* p = parms + 8; *p;) {
+          devs.push_back(atoi(p));
+          while (*p && *p != ',') ++p;
+          if (*p == ',') ++p;
+        }
+      }
+      if (devs.empty()) return nullptr;
+    }
+    if (parms && strcmp(parms, "host") == 0) gpu = false;
     auto* d = new YRTDevice_;
-    d->d = new Device(devId, gpu);
+    d->d = new Device(devs, gpu);
     return d;
   } catch (...) {
     return nullptr;
@@ -1097,12 +1311,13 @@ int yrtPick(YRTDevice dev, YRTHandle camera, float x, float y, YRTHandle scene, 
   auto S = D.get<SceneObj>(scene, "scene");
   if (!C || !S || !S->gpu) throw std::runtime_error("rtPick: invalid camera or uncommitted scene");
   HIP_CHECK(hipSetDevice(D.hipDevice));
-  D.dCam.alloc(sizeof(GpuCamera));
-  D.dCount.alloc(sizeof(float4));
-  HIP_CHECK(hipMemcpyAsync(D.dCam.p, &C->cam, sizeof(GpuCamera), hipMemcpyHostToDevice, D.stream));
-  launch_pick(S->gpu->view, D.dCam.as<GpuCamera>(), x, y, D.dCount.as<float4>(), D.stream);
+  GpuCtx& g = *D.ctx[0];
+  g.dCam.alloc(sizeof(GpuCamera));
+  g.dCount.alloc(sizeof(float4));
+  HIP_CHECK(hipMemcpyAsync(g.dCam.p, &C->cam, sizeof(GpuCamera), hipMemcpyHostToDevice, D.stream));
+  launch_pick(S->gpu->view, g.dCam.as<GpuCamera>(), x, y, g.dCount.as<float4>(), D.stream);
   float4 r;
-  HIP_CHECK(hipMemcpyAsync(&r, D.dCount.p, sizeof(r), hipMemcpyDeviceToHost, D.stream));
+  HIP_CHECK(hipMemcpyAsync(&r, g.dCount.p, sizeof(r), hipMemcpyDeviceToHost, D.stream));
   HIP_CHECK(hipStreamSynchronize(D.stream));
   *px = r.x;
   *py = r.y;
@@ -1235,7 +1450,8 @@ int yrtSetRayCapture(YRTDevice dev, int maxPerDepth) {
 int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* org4, float* dir4, size_t maxRays,
                            double* totalInBatch) {
   DEV_GUARD(dev, -1)
-  auto& v = shadow ? dev->d->capShadow : dev->d->capClosest;
+  if (dev->d->ctx.empty()) throw std::runtime_error("host-only device");
+  auto& v = shadow ? dev->d->ctx[0]->capShadow : dev->d->ctx[0]->capClosest;
   if (depth < 0 || depth >= (int)v.size()) {
     if (totalInBatch) *totalInBatch = 0;
     return 0;
@@ -1265,6 +1481,40 @@ int yrtSetTileShard(YRTDevice dev, int index, int count) {
   dev->d->shardIndex = index;
   dev->d->shardCount = count;
   return 0;
+  DEV_END(-1)
+}
+
+int yrtShardCommUniqueId(void* id128) {
+  try {
+    ncclUniqueId id;
+    rccl_check(rccl().GetUniqueId(&id), "ncclGetUniqueId");
+    memcpy(id128, &id, sizeof(id));
+    return 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128) {
+  DEV_GUARD(dev, -1)
+  Device& D = *dev->d;
+  if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("invalid shard");
+  if (!D.gpu) throw std::runtime_error("host-only device");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  memcpy(&id, id128, sizeof(id));
+  HIP_CHECK(hipSetDevice(D.hipDevice));
+  if (D.procComm) rccl().CommDestroy(D.procComm), D.procComm = nullptr;
+  if (world > 1) rccl_check(rccl().CommInitRank(&D.procComm, world, id, rank), "ncclCommInitRank");
+  D.shardIndex = rank;
+  D.shardCount = world;
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtGetDeviceCount(YRTDevice dev) {
+  DEV_GUARD(dev, -1)
+  return (int)dev->d->ctx.size();
   DEV_END(-1)
 }
 

@@ -36,7 +36,11 @@ static YRTSession session_new(YRTDevice dev, const std::vector<std::string>& arg
   try {
     st.dev = dev;
     if (!st.dev) {
-      st.dev = yrtNewDevice("", 0, 0, "");
+      // every visible GPU unless YRT_DEVICES names them (the DLL's numThreads = 0 -> all
+      // cores default, renderer.cpp:1599-1601), tiles dealt over them
+      const char* e = getenv("YRT_DEVICES");
+      const std::string parms = std::string("devices=") + (e && *e ? e : "all");
+      st.dev = yrtNewDevice(parms.c_str(), 0, 0, "");
       st.ownsDevice = true;
       if (!st.dev) throw std::runtime_error("cannot create the MI355X device (no HIP device?)");
     }

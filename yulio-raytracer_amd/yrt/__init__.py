@@ -33,15 +33,22 @@ def _xfm(t):
 
 
 class Device:
-    """One MI355X (HIP device ``device``) or, with ``host=True``, a host-only device that
-    loads, commits and exports scenes but cannot render (used by the CPU test suite)."""
+    """One MI355X (HIP device ``device``); several (``devices=[0, 1, ...]`` or ``"all"``: the
+    frame's tiles dealt over them, gathered on the first; an id may repeat for logical shards
+    of one GPU); or, with ``host=True``, a host-only device that loads, commits and exports
+    scenes but cannot render (used by the CPU test suite)."""
 
-    def __init__(self, device: int = 0, host: bool = False, handle=None):
+    def __init__(self, device: int = 0, host: bool = False, handle=None, devices=None):
         self._owned = handle is None
         if handle is not None:
             self.h = handle
         else:
-            parms = "host" if host else f"device={device}"
+            if host:
+                parms = "host"
+            elif devices is not None:
+                parms = "devices=" + (devices if isinstance(devices, str) else ",".join(str(int(d)) for d in devices))
+            else:
+                parms = f"device={device}"
             self.h = N.dev.yrtNewDevice(_b(parms), 0, 0, b"")
             if not self.h:
                 raise RuntimeError(f"yrtNewDevice({parms!r}) failed (no HIP device?)")
@@ -344,6 +351,23 @@ class Device:
 
     def set_tile_shard(self, index, count):
         self._rc(N.dev.yrtSetTileShard(self.h, int(index), int(count)), "set_tile_shard")
+
+    def device_count(self) -> int:
+        return int(N.dev.yrtGetDeviceCount(self.h))
+
+    @staticmethod
+    def shard_comm_unique_id() -> bytes:
+        """128-byte RCCL unique id (rank 0), to broadcast to the other ranks."""
+        buf = (C.c_uint8 * 128)()
+        if N.dev.yrtShardCommUniqueId(buf) != 0:
+            raise RuntimeError("yrtShardCommUniqueId failed (librccl unavailable?)")
+        return bytes(buf)
+
+    def set_shard_comm(self, rank, world, uid: bytes):
+        """Tiles dealt round-robin over `world` processes; each frame is gathered on rank 0
+        inside rtRenderFrame (grouped RCCL send/recv, yrtSetShardComm)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._rc(N.dev.yrtSetShardComm(self.h, int(rank), int(world), buf), "set_shard_comm")
 
 
 def sample_table(spp, sets, iteration, num1D, num2D, filter="bspline"):

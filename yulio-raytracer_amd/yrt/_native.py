@@ -143,6 +143,9 @@ _sig(dev, "yrtExportFrame", C.c_int64, vp, vp, vp, vp, vp, sz)
 _sig(dev, "yrtSetFrameSeed", i32, vp, C.c_uint32)
 _sig(dev, "yrtSetBatchCapacity", i32, vp, C.c_int64)
 _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
+_sig(dev, "yrtShardCommUniqueId", i32, vp)
+_sig(dev, "yrtSetShardComm", i32, vp, i32, i32, vp)
+_sig(dev, "yrtGetDeviceCount", i32, vp)
 _sig(dev, "yrtSetRefitCommits", i32, vp, i32)
 _sig(dev, "yrtGetSceneRefits", i32, vp, vp)
 _sig(dev, "yrtSetRayCapture", i32, vp, i32)
