@@ -34,9 +34,13 @@ def c3_args(size=2048, spp=64):
     return ["-i", str(x)] + standin.C3_ARGS + ["-size", str(size), str(size), "-spp", str(spp)]
 
 
-def parity(g: np.ndarray, c: np.ndarray, min_frac: float, mad_rel: float | None = 1e-4, atol=1e-3, rtol=1e-3):
+def parity(g: np.ndarray, c: np.ndarray, min_frac: float, mad_rel: float | None = 1e-4, atol=1e-3, rtol=1e-3,
+           exact: bool = True):
     """per channel |g-c| <= atol + rtol*|c| on >= min_frac of channels, and
-    mean-abs-diff <= mad_rel * mean(c). Returns a dict of the measured quantities."""
+    mean-abs-diff <= mad_rel * mean(c). With exact (the default) the frames must also be
+    bit-identical: the device and the oracle evaluate the same IEEE operations in the same order
+    (no FMA contraction, shared elementary functions yrt_libm.h), so any
+    difference is a defect, not rounding. Returns a dict of the measured quantities."""
     g = np.asarray(g, np.float64)
     c = np.asarray(c, np.float64)
     assert g.shape == c.shape, (g.shape, c.shape)
@@ -50,4 +54,6 @@ def parity(g: np.ndarray, c: np.ndarray, min_frac: float, mad_rel: float | None 
     assert frac >= min_frac, res
     if mad_rel is not None:
         assert mad <= mad_rel * mean + 1e-7, res
+    if exact:
+        assert np.array_equal(g, c), res
     return res

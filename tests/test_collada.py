@@ -122,7 +122,7 @@ def test_dae_fpr_face_parity(gpu_device, tmp_path, cam):
                     device=gpu_device)
     img = s.render_scene_camera(cam)
     ref, _ = oracle.render(s.export_frame(camera=s.scene_camera(cam)), 48, 48, s.info()["gamma"])
-    parity(img, ref, 0.995, mad_rel=None)
+    parity(img, ref, 0.995)
     s.close()
 
 

@@ -60,7 +60,7 @@ def test_materials_lights_parity(gpu_device, depth):
                     device=gpu_device)
     img = s.render()
     ref, _ = oracle.render(s.export_frame(), 96, 72, s.info()["gamma"])
-    parity(img, ref, 0.995, mad_rel=2e-4)
+    parity(img, ref, 0.995)
     s.close()
 
 
@@ -83,5 +83,5 @@ def test_depth_of_field_parity(gpu_device):
                     device=gpu_device)
     img = s.render()
     ref, _ = oracle.render(s.export_frame(), 80, 60, s.info()["gamma"])
-    parity(img, ref, 0.995, mad_rel=2e-4)
+    parity(img, ref, 0.995)
     s.close()

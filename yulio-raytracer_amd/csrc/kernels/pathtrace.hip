@@ -647,13 +647,13 @@ __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 d
 
 __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V3 R, float a = 0.f, float b = 0.f,
                                          float c = 0.f) {
+  (void)type;  // == comp_type(kind), documented at each call
   // Unconditional constant-index stores of selected values: a conditional store lets the
   // optimizer merge the slots into a pointer phi, which pins the set in scratch memory.
 #pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i) {
     const bool w = i == bs.n;
     bs.c[i].kind = w ? kind : bs.c[i].kind;
-    bs.c[i].type = w ? type : bs.c[i].type;
     bs.c[i].R = v3(w ? R.x : bs.c[i].R.x, w ? R.y : bs.c[i].R.y, w ? R.z : bs.c[i].R.z);
     bs.c[i].a = w ? a : bs.c[i].a;
     bs.c[i].b = w ? b : bs.c[i].b;
@@ -935,7 +935,6 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
 #pragma unroll
     for (int k = 0; k < YRT_MAX_COMPS; ++k) {
       bs.c[k].kind = 0;
-      bs.c[k].type = 0;
       bs.c[k].R = v3s(0.f);
       bs.c[k].a = bs.c[k].b = bs.c[k].c = 0.f;
     }
@@ -976,8 +975,10 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         const int g = sv.triGeom[gid];
 #endif
         const int mat = sv.geoms[g].material;
-        const bool wantT = mat >= 0 && ((sv.materials[mat].type == MAT_OBJ && sv.materials[mat].tex[4] >= 0) ||
-                                        (MM & mat_bit(MAT_BRUSHED_METAL) && sv.materials[mat].type == MAT_BRUSHED_METAL));
+        // tangents only feed the Obj bump map and the anisotropic microfacet
+        const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && sv.materials[mat].type == MAT_OBJ &&
+                                         sv.materials[mat].tex[4] >= 0) ||
+                                        ((MM & mat_bit(MAT_BRUSHED_METAL)) && sv.materials[mat].type == MAT_BRUSHED_METAL));
         post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
         bool backfacing = false;
         if (dot(dg.Ng, dir) > 0.f) {
@@ -993,7 +994,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         }
 #pragma unroll
         for (int k = 0; k < YRT_MAX_COMPS; ++k)
-          if (k < bs.n) useDirect |= (bs.c[k].type & BT_DIFFUSE) != 0;
+          if (k < bs.n) useDirect |= (comp_type(bs.c[k].kind) & BT_DIFFUSE) != 0;
       }
     }
 

@@ -77,11 +77,26 @@ __host__ __device__ constexpr unsigned light_bit(int t) { return 1u << (16 + t);
 #define YRT_ALL_LIGHTS 0x7F0000u
 
 struct Comp {
-  int kind;
-  uint32_t type;
+  int kind;  // its BRDF type bits are a function of the kind (comp_type)
   V3 R;
   float a, b, c;
 };
+
+// BRDF type of a component kind (brdfs/*.h constructors): diffuse {Lambertian,
+// DielectricLayer<Lambertian>, Minnaert, Velvety}, specular reflection {DielectricReflection,
+// Reflection, Conductor}, specular transmission {ConstDielectricTransmission,
+// ThinDielectricTransmission, Transmission, DielectricTransmission}, glossy reflection
+// {Microfacet (all three), Specular}
+__device__ __forceinline__ uint32_t comp_type(int kind) {
+  constexpr unsigned kDiff = (1u << C_LAMBERT) | (1u << C_DIEL_LAYER_LAMB) | (1u << C_MINNAERT) | (1u << C_VELVETY);
+  constexpr unsigned kSpecR = (1u << C_DIEL_REFL) | (1u << C_REFLECTION) | (1u << C_CONDUCTOR);
+  constexpr unsigned kSpecT =
+      (1u << C_CONST_DIEL_TRANS) | (1u << C_THIN_DIEL_TRANS) | (1u << C_TRANSMISSION) | (1u << C_DIEL_TRANS);
+  const unsigned b = 1u << kind;
+  return (b & kDiff) ? BT_DIFFUSE_REFLECTION
+                     : (b & kSpecR) ? BT_SPECULAR_REFLECTION
+                                    : (b & kSpecT) ? BT_SPECULAR_TRANSMISSION : BT_GLOSSY_REFLECTION;
+}
 
 #define YRT_MAX_COMPS 3
 
@@ -494,7 +509,7 @@ __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, const GpuMaterial* __r
   V3 c = v3s(0.0f);
 #pragma unroll
   for (int i = 0; i < YRT_MAX_COMPS; ++i)
-    if (i < bs.n && (bs.c[i].type & type)) {
+    if (i < bs.n && (comp_type(bs.c[i].kind) & type)) {
       const Comp ci = bs.c[i];
       c = c + comp_eval<CM>(ci, mats, wo, dg, wi);
     }
@@ -561,14 +576,14 @@ __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, const GpuMaterial* _
   V3 col = colors[0];
   wi_o = dirs[0];
   pdf_o = pdfs[0] * f[0];
-  type_o = bs.c[0].type;
+  type_o = comp_type(bs.c[0].kind);
 #pragma unroll
   for (int i = 1; i < YRT_MAX_COMPS; ++i)
     if (chosen == i) {
       col = colors[i];
       wi_o = dirs[i];
       pdf_o = pdfs[i] * f[i];
-      type_o = bs.c[i].type;
+      type_o = comp_type(bs.c[i].kind);
     }
   return col;
 }
