@@ -1877,16 +1877,18 @@ typedef struct {
   V3 up;
   char filter[16];
   int debug;
+  int backplate; /* image object or -1 (pathtraceintegrator.cpp:32) */
 } RCfg;
 
 /* PathTraceIntegrator::Li (integrators/pathtraceintegrator.cpp:50-217) */
 static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, uint32_t pixelId, int s, uint32_t seed,
-             double* nClosest, double* nShadow) {
+             float pixelX, float pixelY /* state.pixel (integratorrenderer.cpp:162) */, double* nClosest,
+             double* nShadow) {
 #define S1(d) T->t[(size_t)(5 + (d)) * T->rec + rec]
 #define S2X(d) T->t[(size_t)(5 + T->n1 + 2 * (d)) * T->rec + rec]
 #define S2Y(d) T->t[(size_t)(5 + T->n1 + 2 * (d) + 1) * T->rec + rec]
   V3 L = vs(0.f), thr = vs(1.f);
-  int depth = 0, ignoreVL = 0;
+  int depth = 0, ignoreVL = 0, unbent = 1;
   Medium medium = {vs(1.0f), 1.0f}; /* Medium::Vacuum() */
   const float eta = 1.f; /* Sample copy drops eta */
   while (depth < R->maxDepth) {
@@ -1895,7 +1897,15 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     *nClosest += 1;
     const V3 wo = neg(ray.dir);
     if (h.tri < 0) {
-      if (!ignoreVL)
+      if (R->backplate >= 0 && unbent) { /* pathtraceintegrator.cpp:80-84 */
+        const Obj* bp = &W->blob->objs[R->backplate];
+        int bx = (int)(pixelX * (float)bp->imgW), by = (int)(pixelY * (float)bp->imgH);
+        bx = bx < 0 ? 0 : bx > bp->imgW - 1 ? bp->imgW - 1 : bx;
+        by = by < 0 ? 0 : by > bp->imgH - 1 ? bp->imgH - 1 : by;
+        float c[4];
+        img_get(W->blob, R->backplate, bx, by, c);
+        L = add(L, mulv(thr, v3(c[0], c[1], c[2])));
+      } else if (!ignoreVL)
         for (int i = 0; i < W->nenv; i++) {
           const Light* E = &W->lights[W->env[i]];
           V3 Le;
@@ -2001,6 +2011,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     }
     thr = muls(mulv(thr, c), rcp(pdf));
     ignoreVL = (type & BT_DIFFUSE) != 0;
+    unbent = unbent && veq(wi, ray.dir); /* LightPath::extended (pathtraceintegrator.h:45) */
     ray.org = dg.P;
     ray.dir = wi;
     ray.tnear = dg.error * R->epsilon;
@@ -2015,6 +2026,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
 
 static int rcfg_build(const Blob* B, RCfg* R) {
   memset(R, 0, sizeof(*R));
+  R->backplate = -1;
   if (B->renderer < 0) return fail("no renderer");
   const Obj* o = &B->objs[B->renderer];
   if (!strcasecmp(o->type, "debug")) { /* debugrenderer.cpp:21-25 */
@@ -2038,6 +2050,7 @@ static int rcfg_build(const Blob* B, RCfg* R) {
   R->sets = p_int(o, "sampler.sets", 64);
   if (R->sets < 1) R->sets = 1;
   snprintf(R->filter, sizeof(R->filter), "%s", p_str(o, "filter", "bspline"));
+  R->backplate = p_obj(o, "backplate");
   return 0;
 }
 
@@ -2086,7 +2099,7 @@ static void* worker(void* arg) {
                      &ray.dir); /* sample.getLens() */
           ray.tnear = 0.f;
           ray.tfar = INFINITY;
-          L = add(L, Li(J->W, J->R, J->T, rec, ray, (uint32_t)(y * J->width + x), s, J->seed, &nc, &ns));
+          L = add(L, Li(J->W, J->R, J->T, rec, ray, (uint32_t)(y * J->width + x), s, J->seed, fx, fy, &nc, &ns));
         }
         /* AccuBuffer::update + DefaultToneMapper::eval */
         V3 L0 = muls(L, rcp((float)spp));
@@ -2279,6 +2292,10 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
     if (r.tfar >= r.tnear) {
       const V3 inv = v3(safe_inv(r.dir.x), safe_inv(r.dir.y), safe_inv(r.dir.z));
       const float o[3] = {r.org.x, r.org.y, r.org.z}, iv[3] = {inv.x, inv.y, inv.z};
+      /* the kernel's fused slab test (yrt_traverse.h box4_ordered): fma(plane, inv, -org*inv),
+       * far distances widened by 2^-22 * max|org*inv| on top of the robust factor */
+      const float oi[3] = {o[0] * iv[0], o[1] * iv[1], o[2] * iv[2]};
+      const float margin = fmaxf(fmaxf(fabsf(oi[0]), fabsf(oi[1])), fabsf(oi[2])) * 2.384185791015625e-07f;
       int stack[128], sp = 0, cur = 0, done = 0;
       while (!done) {
         if ((cur & 31) == 0) {
@@ -2289,10 +2306,10 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
           for (int k = 0; k < 4; ++k) {
             const float lo[3] = {nd->lox[k], nd->loy[k], nd->loz[k]}, hi[3] = {nd->hix[k], nd->hiy[k], nd->hiz[k]};
             float l[3], h[3];
-            for (int a = 0; a < 3; ++a) { l[a] = (lo[a] - o[a]) * iv[a]; h[a] = (hi[a] - o[a]) * iv[a]; }
+            for (int a = 0; a < 3; ++a) { l[a] = fmaf(lo[a], iv[a], -oi[a]); h[a] = fmaf(hi[a], iv[a], -oi[a]); }
             const float nn = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
             const float ff = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
-            const int hit = nn <= ff * 1.00000036f && nd->child[k] != -1;
+            const int hit = nn <= fmaf(ff, 1.00000036f, margin) && nd->child[k] != -1;
             t[k] = hit ? nn : INF;
             c[k] = nd->child[k];
           }

@@ -182,3 +182,34 @@ def test_face_camera_refit_equals_rebuild(gpu_device, tmp_path):
             gpu_device.set_refit_commits(True)
     for a, b in zip(imgs[True], imgs[False]):
         assert np.array_equal(a, b)
+
+
+def test_rt_test_dll_usage():
+    """The plain-C DLL driver (rt_test_dll/rt_test_dll.cpp counterpart) links against
+    libYulioRT_mi355x.so and prints its usage without a scene (no GPU call)."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "yulio-raytracer_amd" / "lib" / "rt_test_dll"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+@pytest.mark.gpu
+def test_rt_test_dll_renders(tmp_path):
+    """rt_test_dll (C, InitParamsRT -> StartRT -> WaitRT, rt_test_dll.cpp:12-44) renders the
+    Collada scene's FPR views; and with --stop-after it stops a default-size render
+    (StopRT(false): state Stopped, no image kept, :36-39)."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "yulio-raytracer_amd" / "lib" / "rt_test_dll"
+    f = dae_scene.write(tmp_path)
+    r = subprocess.run([str(exe), str(f), "32", "2", "--watermark"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "state Done" in r.stdout
+    assert (tmp_path / "room_Kitchen.jpg").exists() and (tmp_path / "room_Hall.jpg").exists()
+    d2 = tmp_path / "stop"
+    f2 = dae_scene.write(d2)
+    r = subprocess.run([str(exe), str(f2), "--stop-after", "0.5"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "state Stopped" in r.stdout
+    assert not list(d2.glob("room_*.jpg"))

@@ -85,3 +85,34 @@ def test_depth_of_field_parity(gpu_device):
     ref, _ = oracle.render(s.export_frame(), 80, 60, s.info()["gamma"])
     parity(img, ref, 0.995)
     s.close()
+
+
+def test_backplate_oracle(host_device):
+    """-backplate (renderer.cpp:1259-1263; pathtraceintegrator.cpp:80-84): straight camera
+    rays that miss the scene see the backplate at their image-plane position instead of the
+    environment; bent paths still see the environment."""
+    from helpers import c4_args, SCENES
+    base = c4_args(48, 1, stereo=False)
+    s0 = yrt.Session(base + ["-fb", "RGB_FLOAT32"], device=host_device)
+    s1 = yrt.Session(base + ["-backplate", str(SCENES / "logo.png"), "-fb", "RGB_FLOAT32"], device=host_device)
+    objs = dae_scene.blob_objects(s1.export_frame())
+    rend = [o for o in objs if o[0] == "RENDERER"][0]
+    assert "backplate" in rend[2]
+    a, _ = oracle.render(s0.export_frame(), 48, 48, 1.0)
+    b, _ = oracle.render(s1.export_frame(), 48, 48, 1.0)
+    assert not np.array_equal(a, b)
+    s0.close()
+    s1.close()
+
+
+@pytest.mark.gpu
+def test_backplate_parity(gpu_device):
+    """The backplate on the device, bit-identical to the oracle (C4 view: most camera rays
+    leave toward the sky, so the backplate fills the background)."""
+    from helpers import c4_args, SCENES
+    s = yrt.Session(c4_args(96, 4, stereo=False) + ["-backplate", str(SCENES / "lines.ppm"), "-fb", "RGB_FLOAT32"],
+                    device=gpu_device)
+    img = s.render()
+    ref, _ = oracle.render(s.export_frame(), 96, 96, s.info()["gamma"])
+    parity(img, ref, 0.999)
+    s.close()

@@ -61,6 +61,8 @@ struct GpuCtx {
   Lane lanes[kMaxLanes];
   int numLanes = kMaxLanes;
   DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab;
+  DevBuf dBackplate;                       // the renderer's backplate image (texels)
+  const ImageObj* backplateKey = nullptr;  // the image dBackplate holds
   std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
@@ -409,6 +411,20 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
   fv.pixelSets = g.dPixelSets.as<uint8_t>();
   fv.numRecords = tab.numRecords;
   fv.numLightSlots = std::max(1, tab.numLightSlots);
+  memset(&fv.backplate, 0, sizeof(fv.backplate));
+  fv.backplateTexels = nullptr;
+  if (R.backplate && !R.debug) {
+    const ImageObj& im = *R.backplate;
+    if (g.backplateKey != &im || g.dBackplate.bytes < im.data.size()) {
+      g.dBackplate.upload(im.data);
+      g.backplateKey = &im;
+    }
+    fv.backplate.width = im.width;
+    fv.backplate.height = im.height;
+    fv.backplate.format = im.format;
+    fv.backplate.offset = 0;
+    fv.backplateTexels = g.dBackplate.as<uint8_t>();
+  }
 
   if (reportProgress) status(R, 1, 0.f);
   const int numTiles = rp.numTilesX * rp.numTilesY;

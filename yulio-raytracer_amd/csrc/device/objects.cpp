@@ -537,7 +537,8 @@ void RendererObj::commit() {
     filter = parms.getString("filter", "bspline");
     if (filter != "none" && filter != "box" && filter != "bspline")
       throw std::runtime_error("unknown filter type: " + filter);
-    if (parms.getObject("backplate")) throw std::runtime_error("backplate images are not supported by the MI355X device");
+    backplate = std::dynamic_pointer_cast<ImageObj>(parms.getObject("backplate"));
+    if (parms.getObject("backplate") && !backplate) throw std::runtime_error("backplate is not an image");
     stopFlag = (std::atomic<bool>*)parms.getPointer("stopFlag");
     statusCallback = parms.getPointer("statusCallback");
     statusUser = parms.getPointer("statusUser");

@@ -181,6 +181,7 @@ struct RendererObj : Object {
   float minContribution = .02f, epsilon = 32.f * kUlp, tMaxShadowRay = INFINITY, tMaxShadowJitter = .15f;
   V3 up = v3(0.f, 1.f, 0.f);
   std::string filter = "bspline";
+  std::shared_ptr<ImageObj> backplate;  // pathtraceintegrator.cpp:32, used at :80-84
   std::atomic<bool>* stopFlag = nullptr;
   void* statusCallback = nullptr;   // RendererStatusCallback* (C++ ref) or YrtStatusCallback
   void* statusUser = nullptr;

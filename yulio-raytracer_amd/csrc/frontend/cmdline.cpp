@@ -116,6 +116,8 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
       check(dev, yrtSetFloat1(dev, renderer, "tMaxShadowRay", tMaxShadowRay), "rtSetFloat1");
     check(dev, yrtSetInt1(dev, renderer, "sampler.spp", spp), "rtSetInt1");
     if (stopFlag) check(dev, yrtSetStopFlag(dev, renderer, (volatile int*)stopFlag), "stopFlag");
+    // parsePathTracer re-applies g_backplate to the new renderer (renderer.cpp:423)
+    if (backplate && strcmp(type, "debug") != 0) check(dev, yrtSetImage(dev, renderer, "backplate", backplate), "rtSetImage");
     if (statusCallback)
       check(dev, yrtSetStatusCallback(dev, renderer, (YRTStatusCallback)statusCallback, statusUser), "statusCallback");
   };
@@ -285,7 +287,8 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
           else if (t == "spp" && r != "debug") check(dev, yrtSetInt1(dev, renderer, "sampler.spp", cin.getInt()), "rtSetInt1");
           else if (t == "minContribution" && r != "debug")
             check(dev, yrtSetFloat1(dev, renderer, "minContribution", cin.getFloat()), "rtSetFloat1");
-          else if (t == "backplate") throw std::runtime_error("backplate images are outside the MI355X device's scope");
+          else if (t == "backplate" && r != "debug")  // renderer.cpp:435
+            check(dev, yrtSetImage(dev, renderer, "backplate", loader->image(path + cin.get())), "rtSetImage");
           else cin.get();  // unknown tag (reference prints a warning)
         }
         cin.drop();
@@ -318,7 +321,10 @@ void RtState::parseCommandLine(const std::vector<std::string>& tokens, const std
       check(dev, yrtSetInt1(dev, renderer, "sampler.spp", spp), "rtSetInt1");
       check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
     } else if (tag == "-backplate") {
-      throw std::runtime_error("backplate images are outside the MI355X device's scope");
+      // renderer.cpp:1259-1263
+      backplate = loader->image(path + cin.get());
+      check(dev, yrtSetImage(dev, renderer, "backplate", backplate), "rtSetImage");
+      check(dev, yrtCommit(dev, renderer), "rtCommit(renderer)");
     } else if (tag == "-frames") {
       numFrames = cin.getInt();
     } else if (tag == "-o") {

@@ -96,6 +96,7 @@ struct RtState {
   float tMaxShadowRay = INFINITY, tMaxShadowJitter = .2f, sceneScale = 1.f;
   std::string faceCullingMode = "default";
   YRTHandle renderer = nullptr, tonemapper = nullptr, frameBuffer = nullptr, scene = nullptr;
+  YRTHandle backplate = nullptr;  // g_backplate (renderer.cpp:264): kept across renderer re-creation
   std::vector<YRTHandle> prims;
   std::map<int, YRTHandle> cameras;
   std::string sceneType = "default", accel = "default", builder = "default", traverser = "default";

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   } while (0)
   // ray kept as plain vectors across iterations (a loop-carried RayPre struct ends up in
   // scratch: the vectorizer's straddling loads defeat SROA); rebuilt in registers per step
-  float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, ri = ro;
+  float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, ri = ro, rc = ro;
   Hit best;
   best.t = best.u = best.v = 0.f;
   best.tri = -1;
@@ -412,6 +412,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             rd = dir[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
+            {
+              V3 oi;
+              float mg;
+              ray_slab_consts(v3(ro.x, ro.y, ro.z), v3(ri.x, ri.y, ri.z), oi, mg);
+              rc = make_float4(oi.x, oi.y, oi.z, mg);
+            }
             best.t = rd.w;
             best.u = best.v = 0.f;
             best.tri = -1;
@@ -442,6 +448,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     r.inv = v3(ri.x, ri.y, ri.z);
     r.tnear = ro.w;
     r.tfar = rd.w;
+    r.oi = v3(rc.x, rc.y, rc.z);
+    r.margin = rc.w;
 
     // One step per iteration, chosen wave-uniformly ("while-while" with speculative leaf
     // parking, Aila & Laine 2009): node steps while any lane still searches for its first
@@ -825,12 +833,9 @@ __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V
   return r;
 }
 
-// YRT_SHADE_LIGHT_SPEC: the shade instantiation handles only the light types in bits 16.. of
-// its mask (LM = bit LIGHT_x); 0 = every type.
-#ifndef YRT_SHADE_LIGHT_SPEC
-#define YRT_SHADE_LIGHT_SPEC 0  // measured neutral-to-worse on C3 (A/B), kept off
-#endif
-#define YRT_LM(MM) (YRT_SHADE_LIGHT_SPEC ? ((MM) >> 16) : 0x7Fu)
+// LM: the light types (bit LIGHT_x) an instantiation handles; the shade kernel uses every type
+// (specializing per scene light set measured neutral-to-worse on C3).
+constexpr unsigned kAllLights = 0x7Fu;
 template <unsigned LM>
 __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
   if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
@@ -962,12 +967,26 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       const int gid = __float_as_int(h.w);
       isHit = gid >= 0;
       if (!isHit) {
-        // environment shading (pathtraceintegrator.cpp:79-92); backplate not supported
-        if (!ignoreVL)
+        // environment shading (pathtraceintegrator.cpp:79-92): the backplate for a straight
+        // camera ray, looked up at the sample's image-plane position (state.pixel)
+        if (fv.backplateTexels && unbent) {
+          const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
+          const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
+          const GpuImage& bp = fv.backplate;
+          const int bx = max(0, min((int)(fx * (float)bp.width), bp.width - 1));
+          const int by = max(0, min((int)(fy * (float)bp.height), bp.height - 1));
+          float c[4];
+          texel(bp, fv.backplateTexels, bx, by, c);
+          const float4 l4 = pb.pathL[path];
+          L = v3(l4.x, l4.y, l4.z);
+          haveL = true;
+          L = L + thr * v3(c[0], c[1], c[2]);
+        } else if (!ignoreVL) {
           for (int j = 0; j < sv.numEnvLights; ++j) {
             if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
-            L = L + thr * env_Le<YRT_LM(MM)>(sv, sv.lights[sv.envLights[j]], wo);
+            L = L + thr * env_Le<kAllLights>(sv, sv.lights[sv.envLights[j]], wo);
           }
+        }
       } else {
 #if YRT_SHADE_FLAT
         const int g = sv.indices[gid].w;
@@ -1066,7 +1085,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
           } else {
             const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
             const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
-            Ls = light_sample<YRT_LM(MM)>(lt, dg, sx, sy, wi, pdf);
+            Ls = light_sample<kAllLights>(lt, dg, sx, sy, wi, pdf);
           }
           if (!(Ls == v3s(0.f) || pdf == 0.f)) {
             const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);

@@ -47,6 +47,8 @@ struct FrameView {
   const float* lightSamples;   // [numRecords][numLightSlots][8]
   const uint8_t* pixelSets;    // W*H set index per pixel
   int numRecords, numLightSlots;
+  GpuImage backplate;           // PathTraceIntegrator backplate (offset 0 in backplateTexels)
+  const uint8_t* backplateTexels;  // null: none
 };
 
 // Queues are split into YRT_QSEGS segments, each with its own append counter on its own

@@ -520,6 +520,7 @@ __device__ __forceinline__ V3 set_eval(const BRDFSet& bs, const GpuMaterial* __r
 // (f_i = sum(c_i)/pdf_i over the components that sampled something, normalized by their
 // running sum, CDF with the last entry forced to 1), written with compile-time component
 // indices only so nothing is spilled to scratch.
+
 template <unsigned CM>
 __device__ __forceinline__ V3 set_sample(const BRDFSet& bs, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
                                          float sx, float sy, float ss, V3& wi_o, float& pdf_o, uint32_t& type_o) {

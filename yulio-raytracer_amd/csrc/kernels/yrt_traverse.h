@@ -53,7 +53,15 @@ __device__ __forceinline__ float safe_inv(float d) {
 struct RayPre {
   V3 org, dir, inv;
   float tnear, tfar;
+  V3 oi;         // org * inv (rounded): slab distances as fma(plane, inv, -oi) (box4_ordered)
+  float margin;  // absolute slack of those distances: 2^-22 * max |oi| (see box4_ordered)
 };
+
+// Per-ray constants of box4_ordered's fused slab test.
+__device__ __forceinline__ void ray_slab_consts(const V3& org, const V3& inv, V3& oi, float& margin) {
+  oi = v3(org.x * inv.x, org.y * inv.y, org.z * inv.z);
+  margin = fmaxf(fmaxf(fabsf(oi.x), fabsf(oi.y)), fabsf(oi.z)) * 2.384185791015625e-07f;  // 2^-22
+}
 
 // Entry distances of the four children of a 4-wide node (INFINITY = missed / empty slot).
 // Slab distances (b - o) * inv are computed two children at a time with packed ops
@@ -112,21 +120,29 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
   const float4 ny = *(const float4*)(b0 + (nb + (32u + oy))), fy = *(const float4*)(b0 + (nb + (48u - oy)));
   const float4 nz = *(const float4*)(b0 + (nb + (64u + oz))), fz = *(const float4*)(b0 + (nb + (80u - oz)));
   const int4 ch = *(const int4*)(b0 + (nb + 96u));
-  const f2 ox2 = {r.org.x, r.org.x}, oy2 = {r.org.y, r.org.y}, oz2 = {r.org.z, r.org.z};
+  // slab distance t = fma(plane, inv, -org*inv): one fused op per plane instead of a subtract
+  // and a multiply. Against (plane - org) * inv it carries an extra absolute error of at most
+  // one rounding of org*inv (u * |oi|, u = 2^-24) on each of the near and far distances; the
+  // far plane is widened by margin = 4u * max|oi| on top of the robust factor (relative
+  // errors, as before), so the test stays conservative: a box the ray meets is never culled,
+  // and the closest hit (smallest (t, triangle id)) is the same for any visit order.
   const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
-  const f2 nx01 = (f2{nx.x, nx.y} - ox2) * ix, nx23 = (f2{nx.z, nx.w} - ox2) * ix;
-  const f2 fx01 = (f2{fx.x, fx.y} - ox2) * ix, fx23 = (f2{fx.z, fx.w} - ox2) * ix;
-  const f2 ny01 = (f2{ny.x, ny.y} - oy2) * iy, ny23 = (f2{ny.z, ny.w} - oy2) * iy;
-  const f2 fy01 = (f2{fy.x, fy.y} - oy2) * iy, fy23 = (f2{fy.z, fy.w} - oy2) * iy;
-  const f2 nz01 = (f2{nz.x, nz.y} - oz2) * iz, nz23 = (f2{nz.z, nz.w} - oz2) * iz;
-  const f2 fz01 = (f2{fz.x, fz.y} - oz2) * iz, fz23 = (f2{fz.z, fz.w} - oz2) * iz;
+  const f2 mx = {-r.oi.x, -r.oi.x}, my = {-r.oi.y, -r.oi.y}, mz = {-r.oi.z, -r.oi.z};
+#define YRT_SLAB(P, I, M, O) __builtin_elementwise_fma(P, I, M)
+  const f2 nx01 = YRT_SLAB((f2{nx.x, nx.y}), ix, mx, ox2), nx23 = YRT_SLAB((f2{nx.z, nx.w}), ix, mx, ox2);
+  const f2 fx01 = YRT_SLAB((f2{fx.x, fx.y}), ix, mx, ox2), fx23 = YRT_SLAB((f2{fx.z, fx.w}), ix, mx, ox2);
+  const f2 ny01 = YRT_SLAB((f2{ny.x, ny.y}), iy, my, oy2), ny23 = YRT_SLAB((f2{ny.z, ny.w}), iy, my, oy2);
+  const f2 fy01 = YRT_SLAB((f2{fy.x, fy.y}), iy, my, oy2), fy23 = YRT_SLAB((f2{fy.z, fy.w}), iy, my, oy2);
+  const f2 nz01 = YRT_SLAB((f2{nz.x, nz.y}), iz, mz, oz2), nz23 = YRT_SLAB((f2{nz.z, nz.w}), iz, mz, oz2);
+  const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz, oz2), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz, oz2);
+#undef YRT_SLAB
   const float INF = __int_as_float(0x7f800000);
-#define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                 \
-  do {                                                                           \
-    const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                   \
-    const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                      \
-    t[k] = nn <= ff * YRT_BOX_ROBUST ? nn : INF;                                 \
-    c[k] = (CH);                                                                 \
+#define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                    \
+  do {                                                                              \
+    const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                      \
+    const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                         \
+    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : INF;           \
+    c[k] = (CH);                                                                    \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
   YRT_CHILD(1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y, ch.y);
