@@ -2313,14 +2313,29 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
             t[k] = hit ? nn : INF;
             c[k] = nd->child[k];
           }
-          /* 5-comparator sort network, as the kernel's sort4; any-hit rays keep slot order
-           * (kernel YRT_CHILD_ORDER 3) */
+          /* 5-comparator sort network, as the kernel's sort4; any-hit rays take the farthest
+           * hit child first, the others in slot order (the kernel's sort3_far: descending
+           * comparators (0,1), (2,3), (0,2) with misses at -INF) */
           static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
-          for (int m = 0; m < (anyHit ? 0 : 5); ++m) {
-            const int a = net[m][0], b = net[m][1];
-            if (t[b] < t[a]) {
-              const float tt = t[a]; t[a] = t[b]; t[b] = tt;
-              const int cc = c[a]; c[a] = c[b]; c[b] = cc;
+          if (anyHit) {
+            for (int k = 0; k < 4; ++k)
+              if (!(t[k] < INF)) t[k] = -INF;
+            for (int m = 0; m < 3; ++m) {
+              const int a = net[m][0], b = net[m][1];
+              if (t[b] > t[a]) {
+                const float tt = t[a]; t[a] = t[b]; t[b] = tt;
+                const int cc = c[a]; c[a] = c[b]; c[b] = cc;
+              }
+            }
+            for (int k = 0; k < 4; ++k)
+              if (t[k] == -INF) t[k] = INF;
+          } else {
+            for (int m = 0; m < 5; ++m) {
+              const int a = net[m][0], b = net[m][1];
+              if (t[b] < t[a]) {
+                const float tt = t[a]; t[a] = t[b]; t[b] = tt;
+                const int cc = c[a]; c[a] = c[b]; c[b] = cc;
+              }
             }
           }
           if (t[3] < INF) stack[sp++] = c[3];

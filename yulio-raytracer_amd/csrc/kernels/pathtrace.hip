@@ -284,11 +284,18 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 #ifndef YRT_REFILL
 #define YRT_REFILL 40  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6
 #endif
-#ifdef YRT_PROFILE
-// [0] outer iterations x waves, [1] lanes holding a ray at outer iterations,
+#if defined(YRT_PROFILE) && defined(YRT_SHADE_PROF)
+#error "YRT_PROFILE and YRT_SHADE_PROF share the profile counters: build one at a time"
+#endif
+#if defined(YRT_PROFILE) || defined(YRT_SHADE_PROF)
+// YRT_PROFILE: [0] outer iterations x waves, [1] lanes holding a ray at outer iterations,
 // [2] node-phase iterations, [3] lanes visiting a node, [4] leaf passes with work,
 // [5] triangle-loop iterations (max leaf size per pass), [6] useful triangle tests
+// YRT_SHADE_PROF: [0..6] k_shade shader-clock cycles per phase summed over waves, [7] wave
+// iterations (see k_shade)
 __device__ unsigned long long g_traceProfile[8];
+#endif
+#ifdef YRT_PROFILE
 #define YRT_PROF(i, v) prof[i] += (unsigned long long)(v)
 #else
 #define YRT_PROF(i, v) ((void)0)
@@ -469,33 +476,35 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         float t[4];
         int c[4];
         // sign-ordered slab planes (+1.5 % on C3 with two lanes, bit-identical distances)
-        box4_ordered(r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
-        // closest-hit rays sort the hit children by entry distance; shadow (any-hit) rays
-        // take them in the builder's slot order — front-to-back order buys an any-hit ray
-        // nothing, and skipping the 5-comparator network cut k_trace<true> by 9 % (profiles/r01)
+        box4_ordered<ANY>(r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
+        // closest-hit rays sort the hit children by entry distance (nearest next, the others
+        // pushed farthest-first); any-hit rays take the farthest hit child next and push the
+        // others in slot order (sort3_far: -22 % node visits against slot order)
         if (!ANY) sort4(t, c);
-        // nearest hit child next; the other hits pushed farthest-first
-        const float INF = __int_as_float(0x7f800000);
+        else sort3_far(t, c);
+        const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
+#define YRT_HIT(x) (ANY ? (x) > MISS : (x) < MISS)
         if (sp + 3 <= YRT_LDS_STACK) {
           // all three candidates fit in free ring slots: store unconditionally, advance sp
           // only past the hit ones (a store of a missed child lands on a free slot);
           // shadow rays -4..9 %, closest neutral (profiles/r01)
-          const int h3 = t[3] < INF, h2 = t[2] < INF, h1 = t[1] < INF;
+          const int h3 = YRT_HIT(t[3]), h2 = YRT_HIT(t[2]), h1 = YRT_HIT(t[1]);
           stack[YRT_SLOT(sp)] = c[3];
           stack[YRT_SLOT(sp + h3)] = c[2];
           stack[YRT_SLOT(sp + h3 + h2)] = c[1];
           sp += h3 + h2 + h1;
         } else {
-          if (t[3] < INF) YRT_PUSH(c[3]);
-          if (t[2] < INF) YRT_PUSH(c[2]);
-          if (t[1] < INF) YRT_PUSH(c[1]);
+          if (YRT_HIT(t[3])) YRT_PUSH(c[3]);
+          if (YRT_HIT(t[2])) YRT_PUSH(c[2]);
+          if (YRT_HIT(t[1])) YRT_PUSH(c[1]);
         }
-        if (t[0] < INF) {
+        if (YRT_HIT(t[0])) {
           curIdx = c[0] >> 5;
           curCnt = c[0] & 31;
         } else {
           YRT_POP();
         }
+#undef YRT_HIT
         if (curCnt > 0 && pendCnt == 0) {
           pendIdx = curIdx;
           pendCnt = curCnt;
@@ -915,6 +924,28 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
 template <unsigned MM>
 __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
+#ifdef YRT_SHADE_PROF
+  // shader-clock cycles per phase (wave-uniform points only), summed over the waves
+  unsigned long long sprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#define SPROF_AT(k)                                            \
+  do {                                                         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    sprof[k] += t_ - tprev;                                    \
+    tprev = t_;                                                \
+  } while (0)
+#endif
+  // YRT_SHADE_PROF=1: one slot per phase; =2: the continuation and direct-light phases split
+#if defined(YRT_SHADE_PROF) && YRT_SHADE_PROF == 1
+#define SPROF_MARK(k) SPROF_AT(k)
+#else
+#define SPROF_MARK(k) ((void)0)
+#endif
+#if defined(YRT_SHADE_PROF) && YRT_SHADE_PROF == 2
+#define SPROF_FINE(k) SPROF_AT(k)
+#else
+#define SPROF_FINE(k) ((void)0)
+#endif
   const GpuRenderParams& rp = *fv.rp;
   __shared__ QMap qm;
   qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
@@ -944,6 +975,9 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       bs.c[k].a = bs.c[k].b = bs.c[k].c = 0.f;
     }
     V3 wo = v3s(0.f);
+    int px = 0, py = 0;
+    SPROF_MARK(7);
+    SPROF_FINE(7);
     if (active) {
       path = pb.qPath[cur][q];
       const float4 o = pb.qOrg[cur][q], d = pb.qDir[cur][q];
@@ -959,14 +993,16 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       medium = (meta >> 10) & 0xFFFF;  // LightPath::lastMedium as a medium-table index
       s = path / bi.numPixels;
       const int i = path - s * bi.numPixels;
-      int x = 0, y = 0;
-      batch_pixel(rp, bi, i, x, y);
-      pixelId = y * rp.width + x;
+      batch_pixel(rp, bi, i, px, py);
+      pixelId = py * rp.width + px;
       rec = fv.pixelSets[pixelId] * rp.spp + s;
       wo = -dir;
-      const int gid = __float_as_int(h.w);
-      isHit = gid >= 0;
-      if (!isHit) {
+      isHit = __float_as_int(h.w) >= 0;
+    }
+    SPROF_MARK(0);  // queue record, pixel and sample record
+    if (active && !isHit) {
+      {
+        const int x = px, y = py;
         // environment shading (pathtraceintegrator.cpp:79-92): the backplate for a straight
         // camera ray, looked up at the sample's image-plane position (state.pixel)
         if (fv.backplateTexels && unbent) {
@@ -987,40 +1023,49 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
             L = L + thr * env_Le<kAllLights>(sv, sv.lights[sv.envLights[j]], wo);
           }
         }
-      } else {
-#if YRT_SHADE_FLAT
-        const int g = sv.indices[gid].w;
-#else
-        const int g = sv.triGeom[gid];
-#endif
-        const int mat = sv.geoms[g].material;
-        // tangents only feed the Obj bump map and the anisotropic microfacet
-        const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && sv.materials[mat].type == MAT_OBJ &&
-                                         sv.materials[mat].tex[4] >= 0) ||
-                                        ((MM & mat_bit(MAT_BRUSHED_METAL)) && sv.materials[mat].type == MAT_BRUSHED_METAL));
-        post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
-        bool backfacing = false;
-        if (dot(dg.Ng, dir) > 0.f) {
-          backfacing = true;
-          dg.Ng = -dg.Ng;
-          dg.Ns = -dg.Ns;
-        }
-        if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg.material, medium, dg, bs);
-        if (!ignoreVL && dg.light >= 0 && !backfacing) {
-          const GpuLight& al = sv.lights[dg.light];
-          if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
-          L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
-        }
-#pragma unroll
-        for (int k = 0; k < YRT_MAX_COMPS; ++k)
-          if (k < bs.n) useDirect |= (comp_type(bs.c[k].kind) & BT_DIFFUSE) != 0;
       }
     }
+    SPROF_MARK(1);  // misses: environment / backplate
+    bool backfacing = false;
+    if (active && isHit) {
+      const int gid = __float_as_int(h.w);
+#if YRT_SHADE_FLAT
+      const int g = sv.indices[gid].w;
+#else
+      const int g = sv.triGeom[gid];
+#endif
+      const int mat = sv.geoms[g].material;
+      // tangents only feed the Obj bump map and the anisotropic microfacet
+      const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && sv.materials[mat].type == MAT_OBJ &&
+                                       sv.materials[mat].tex[4] >= 0) ||
+                                      ((MM & mat_bit(MAT_BRUSHED_METAL)) && sv.materials[mat].type == MAT_BRUSHED_METAL));
+      post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
+      if (dot(dg.Ng, dir) > 0.f) {
+        backfacing = true;
+        dg.Ng = -dg.Ng;
+        dg.Ns = -dg.Ns;
+      }
+    }
+    SPROF_MARK(2);  // postIntersect
+    if (active && isHit) {
+      if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg.material, medium, dg, bs);
+      if (!ignoreVL && dg.light >= 0 && !backfacing) {
+        const GpuLight& al = sv.lights[dg.light];
+        if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
+        L = L + thr * v3(al.L[0], al.L[1], al.L[2]);
+      }
+#pragma unroll
+      for (int k = 0; k < YRT_MAX_COMPS; ++k)
+        if (k < bs.n) useDirect |= (comp_type(bs.c[k].kind) & BT_DIFFUSE) != 0;
+    }
+    SPROF_MARK(3);  // material::shade (textures), emission
 
     // continuation (pathtraceintegrator.cpp:169-213)
     bool cont = false;
     V3 nwi = v3s(0.f), nthr = v3s(0.f);
     int nmeta = 0;
+    bool doSample = false;
+    float sx = 0.f, sy = 0.f, ss = 0.f;
     if (active && isHit) {
       bool stop = depth >= rp.maxDepth - 1;
       if (!stop && rp.rrDepth > 0 && depth >= rp.rrDepth - 1) {  // size_t compare in the reference
@@ -1029,12 +1074,23 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       }
       if (!stop) {
         const int d2 = rp.firstScatterSampleID + depth;
-        const float sx = samp(fv, 5 + rp.dim1D + 2 * d2, rec);
-        const float sy = samp(fv, 5 + rp.dim1D + 2 * d2 + 1, rec);
-        const float ss = samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec);
-        float pdf;
-        uint32_t type;
-        V3 c = set_sample<comps_of(MM)>(bs, sv.materials, wo, dg, sx, sy, ss, nwi, pdf, type);
+        sx = samp(fv, 5 + rp.dim1D + 2 * d2, rec);
+        sy = samp(fv, 5 + rp.dim1D + 2 * d2 + 1, rec);
+        ss = samp(fv, 5 + rp.firstScatterTypeSampleID + depth, rec);
+        doSample = true;
+      }
+    }
+    SPROF_FINE(0);  // everything before CompositedBRDF::sample
+    float spdf = 0.f;
+    uint32_t stype = 0;
+    V3 sc = v3s(0.f);
+    if (doSample) sc = set_sample<comps_of(MM)>(bs, sv.materials, wo, dg, sx, sy, ss, nwi, spdf, stype);
+    SPROF_FINE(1);  // CompositedBRDF::sample
+    if (doSample) {
+      {
+        V3 c = sc;
+        const float pdf = spdf;
+        const uint32_t type = stype;
         if (!(c == v3s(0.f) || pdf <= 0.f)) {
           if (MM & mat_bit(MAT_DIELECTRIC)) {
             // simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207)
@@ -1056,6 +1112,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         }
       }
     }
+    SPROF_MARK(4);  // continuation: CompositedBRDF::sample, Russian roulette
     bool got;
     const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
     if (haveL) pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);
@@ -1065,6 +1122,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
       pb.qThr[cur ^ 1][nq] = make_float4(nthr.x, nthr.y, nthr.z, __int_as_float(nmeta));
     }
+    SPROF_MARK(5);  // continuation append and stores
+    SPROF_FINE(2);  // rest of the continuation, append and stores
 
     // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); its
     // contribution is added to pathL[path] after the emission above (reference order)
@@ -1072,39 +1131,41 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
       bool pred = false;
       V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
       float tnear = 0.f, tfar = 0.f;
-      if (active && isHit && useDirect) {
-        const GpuLight& lt = sv.lights[li];
-        if ((lt.illumMask & dg.illumMask) != 0) {
-          V3 Ls;
-          float pdf;
-          if (lt.precomputed >= 0) {
-            const float* ls = fv.lightSamples + ((size_t)rec * fv.numLightSlots + lt.precomputed) * 8;
-            wi = v3(ls[0], ls[1], ls[2]);
-            pdf = ls[3];
-            Ls = v3(ls[4], ls[5], ls[6]);
-          } else {
-            const float sx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
-            const float sy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
-            Ls = light_sample<kAllLights>(lt, dg, sx, sy, wi, pdf);
-          }
-          if (!(Ls == v3s(0.f) || pdf == 0.f)) {
-            const V3 brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
-            if (!(brdf == v3s(0.f))) {
-              const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
-              const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
-                                                  rp.tMaxShadowRay * rp.tMaxShadowJitter;
-              float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
-              const float dotProduct = dot(wi, ld3(rp.up));
-              if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
-              sOrg = dg.P;
-              tnear = dg.error * rp.epsilon;
-              tfar = tMax - dg.error * rp.epsilon;
-              contrib = thr * Ls * brdf * rcpf_(pdf);
-              pred = true;
-            }
-          }
+      const GpuLight& lt = sv.lights[li];
+      const bool lit = active && isHit && useDirect && (lt.illumMask & dg.illumMask) != 0;
+      V3 Ls = v3s(0.f);
+      float pdf = 0.f;
+      if (lit) {
+        if (lt.precomputed >= 0) {
+          const float* ls = fv.lightSamples + ((size_t)rec * fv.numLightSlots + lt.precomputed) * 8;
+          wi = v3(ls[0], ls[1], ls[2]);
+          pdf = ls[3];
+          Ls = v3(ls[4], ls[5], ls[6]);
+        } else {
+          const float lsx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
+          const float lsy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
+          Ls = light_sample<kAllLights>(lt, dg, lsx, lsy, wi, pdf);
         }
       }
+      SPROF_FINE(3);  // Light::sample
+      const bool lsOk = lit && !(Ls == v3s(0.f) || pdf == 0.f);
+      V3 brdf = v3s(0.f);
+      if (lsOk) brdf = set_eval<comps_of(MM)>(bs, sv.materials, wo, dg, wi, BT_DIFFUSE);
+      SPROF_FINE(4);  // CompositedBRDF::eval
+      if (lsOk && !(brdf == v3s(0.f))) {
+        const float r01 = hash_u01(rp.frameSeed, (uint32_t)pixelId, (uint32_t)s, (uint32_t)(depth * 64 + li));
+        const float shadowRayJitterLength = 2.f * rp.tMaxShadowRay * rp.tMaxShadowJitter * r01 -
+                                            rp.tMaxShadowRay * rp.tMaxShadowJitter;
+        float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
+        const float dotProduct = dot(wi, ld3(rp.up));
+        if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
+        sOrg = dg.P;
+        tnear = dg.error * rp.epsilon;
+        tfar = tMax - dg.error * rp.epsilon;
+        contrib = thr * Ls * brdf * rcpf_(pdf);
+        pred = true;
+      }
+      SPROF_FINE(5);  // shadow-ray jitter, contribution
       bool sgot;
       const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
       if (sgot) {
@@ -1113,9 +1174,14 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
       }
       if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numLights + li] = sgot ? (int)si : -1;
+      SPROF_FINE(6);  // shadow-ray append and stores
     }
-
+    SPROF_MARK(6);  // direct light: light sample, BRDF eval, shadow-ray append and stores
   }
+#ifdef YRT_SHADE_PROF
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_traceProfile[k], sprof[k]);
+#endif
 }
 
 // Adds the unoccluded direct-light terms in light order.
@@ -1437,7 +1503,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_pick(SceneView sv, const Gp
 }
 
 int trace_profile(unsigned long long* out8, int reset) {
-#ifdef YRT_PROFILE
+#if defined(YRT_PROFILE) || defined(YRT_SHADE_PROF)
   if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_traceProfile), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
   if (reset) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -109,6 +109,9 @@ __device__ __forceinline__ int plane_offsets(float ix, float iy, float iz) {
 // child load address the node array as a uniform (SGPR) base plus a 32-bit per-lane byte
 // offset (global_load saddr form) instead of six 64-bit per-lane pointers (78/74 VGPRs instead
 // of 82/84). nodeIdx < 2^25 (node byte offsets fit 32 bits; bvh_build.cpp enforces it).
+// MISS: the entry distance reported for a missed child (+INF for closest-hit rays, which sort
+// ascending; -INF for any-hit rays, which visit the farthest child first, see sort3_far).
+template <bool ANY = false>
 __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
                                              const GpuNode* __restrict__ base, int nodeIdx) {
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -136,12 +139,12 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
   const f2 nz01 = YRT_SLAB((f2{nz.x, nz.y}), iz, mz, oz2), nz23 = YRT_SLAB((f2{nz.z, nz.w}), iz, mz, oz2);
   const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz, oz2), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz, oz2);
 #undef YRT_SLAB
-  const float INF = __int_as_float(0x7f800000);
+  const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
 #define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                    \
   do {                                                                              \
     const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                      \
     const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                         \
-    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : INF;           \
+    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;          \
     c[k] = (CH);                                                                    \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
@@ -168,6 +171,28 @@ __device__ __forceinline__ void sort4(float t[4], int c[4]) {
   YRT_CSWAP(1, 3);
   YRT_CSWAP(1, 2);
 #undef YRT_CSWAP
+}
+
+// Any-hit (shadow) rays: the farthest hit child first, the others in slot order — three
+// descending comparators (0,1), (2,3), (0,2) move the largest entry distance to slot 0
+// (misses are -INF). A shadow ray leaves a surface toward the light: what occludes it lies
+// far along the ray, the children near its origin rarely do. On the C3 shadow-ray streams
+// (tools/visit_order_exp.py): 7.96 node visits and 1.50 triangle tests per ray against 10.25
+// and 1.94 in slot order, 12.5 / 2.46 nearest-first.
+__device__ __forceinline__ void sort3_far(float t[4], int c[4]) {
+#define YRT_CSWAP_D(a, b)                        \
+  do {                                           \
+    const bool sw = t[b] > t[a];                 \
+    const float ta = sw ? t[b] : t[a];           \
+    const float tb = sw ? t[a] : t[b];           \
+    const int ca = sw ? c[b] : c[a];             \
+    const int cb = sw ? c[a] : c[b];             \
+    t[a] = ta; t[b] = tb; c[a] = ca; c[b] = cb;  \
+  } while (0)
+  YRT_CSWAP_D(0, 1);
+  YRT_CSWAP_D(2, 3);
+  YRT_CSWAP_D(0, 2);
+#undef YRT_CSWAP_D
 }
 
 // One triangle; returns true and t when the ray hits within (tnear, tfar). U, V, absDen are
