@@ -205,6 +205,10 @@ YRT_API int64_t yrtGetCapturedRays(YRTDevice dev, int shadow, int depth, float* 
  * reset (outer iterations, lanes with a ray, node-phase iterations, lanes at a node, leaf
  * passes, triangle-loop iterations, useful triangle tests, 0). Returns -1 otherwise. */
 YRT_API int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset);
+/* Arithmetic self-check on the device: fn 0 compares the kernels' correctly rounded fast
+ * reciprocal (rcp_rn, common/yrt_math.h) with the IEEE division 1.0f/x for all 2^32 inputs.
+ * out2[0] = mismatches, out2[1] = the smallest mismatching input (or UINT64_MAX). */
+YRT_API int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2);
 /* Decoder check: 8-bit pixels of a .jpg/.png in file row order (top row first), before the
  * Image4c flip/requantization of rtNewImageFromFile. Call with out=NULL to get the size. */
 YRT_API int yrtDebugDecodeImage(const char* file, int* width, int* height, int* channels, uint8_t* out,

@@ -39,6 +39,18 @@ def test_debug_renderer_bit_exact(gpu_device, args):
     assert np.array_equal(img, ref), np.argwhere(img != ref)[:5]
 
 
+# ----------------------------------------------------------------------------- arithmetic
+def test_fast_reciprocal_is_correctly_rounded(gpu_device):
+    """The kernels' rcp_rn (v_rcp_f32 + one FMA Newton step, IEEE division outside
+    [2^-124, 2^124)) equals the IEEE division 1.0f/x for all 2^32 inputs, so shading stays
+    bit-exact with the oracle's 1/x."""
+    import ctypes as C
+    from yrt import _native as N
+    out = (C.c_uint64 * 2)()
+    assert N.dev.yrtDebugCheckMath(gpu_device.h, 0, out) == 0, gpu_device.error()
+    assert out[0] == 0, f"{out[0]} mismatches, first input bits {out[1]:#x}"
+
+
 # ----------------------------------------------------------------------------- ray queries
 def _rays(blob, n, seed=42):
     """SURVEY §8(d)(ii) incoherent rays: origins uniform in the scene AABB, directions on S^2."""

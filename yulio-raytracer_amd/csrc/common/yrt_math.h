@@ -46,8 +46,31 @@ YRT_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 YRT_HD V3 cross(V3 a, V3 b) {
   return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+#if defined(__HIPCC__)
+// Correctly rounded 1/x without the general division sequence (v_div_scale x2, v_rcp, 5 FMAs,
+// v_div_fmas, v_div_fixup): the hardware reciprocal estimate refined by one FMA Newton step
+// (e = 1 - x*y, y += y*e) is RN(1/x) for every |x| in [2^-124, 2^124) — verified on gfx950
+// for all 2^32 inputs against 1.0f/x (yrtDebugCheckMath, tests/test_gpu_parity.py); zero,
+// subnormal, huge, infinite and NaN inputs take the IEEE division. Same bits as the host's
+// 1/x, so the oracle stays bit-exact.
+__host__ __device__ __forceinline__ float rcp_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float y = __builtin_amdgcn_rcpf(x);
+  const float e = __builtin_fmaf(-x, y, 1.0f);
+  y = __builtin_fmaf(e, y, y);
+  const unsigned ex = (__float_as_uint(x) >> 23) & 0xffu;
+  if (__builtin_expect(ex - 3u > 247u, 0)) y = 1.0f / x;
+  return y;
+#else
+  return 1.0f / x;
+#endif
+}
+YRT_HD float rcpf_(float x) { return rcp_rn(x); }
+YRT_HD float rsqrtf_(float x) { return rcp_rn(sqrtf(x)); }
+#else
 YRT_HD float rcpf_(float x) { return 1.0f / x; }
 YRT_HD float rsqrtf_(float x) { return 1.0f / sqrtf(x); }
+#endif
 YRT_HD V3 normalize(V3 a) { return a * rsqrtf_(dot(a, a)); }
 YRT_HD float length(V3 a) { return sqrtf(dot(a, a)); }
 YRT_HD float reduce_max(V3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }

@@ -1491,6 +1491,15 @@ int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset) {
   DEV_END(-1)
 }
 
+int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2) {
+  DEV_GUARD(dev, -1)
+  if (fn != 0 || !out2) throw std::runtime_error("yrtDebugCheckMath: fn 0 only");
+  HIP_CHECK(hipSetDevice(dev->d->hipDevice));
+  if (check_math(fn, (unsigned long long*)out2) != 0) throw std::runtime_error("check_math failed");
+  return 0;
+  DEV_END(-1)
+}
+
 int yrtSetTileShard(YRTDevice dev, int index, int count) {
   DEV_GUARD(dev, -1)
   if (count < 1 || index < 0 || index >= count) throw std::runtime_error("invalid shard");

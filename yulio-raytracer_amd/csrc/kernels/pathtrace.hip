@@ -859,7 +859,7 @@ template <unsigned LM>
 __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
   if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) {
     // lights/ambientlight.h:52-65 (the bsphere tMax is overwritten by the integrator)
-    wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+    wi = cosine_hemi_dg(sx, sy, dg, pdf);
     return v3(lt.L[0], lt.L[1], lt.L[2]);
   }
   if ((LM & (1u << LIGHT_TRIANGLE)) && lt.type == LIGHT_TRIANGLE) {
@@ -1057,6 +1057,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
 #pragma unroll
       for (int k = 0; k < YRT_MAX_COMPS; ++k)
         if (k < bs.n) useDirect |= (comp_type(bs.c[k].kind) & BT_DIFFUSE) != 0;
+      dg_frame(dg);
     }
     SPROF_MARK(3);  // material::shade (textures), emission
 
@@ -1500,6 +1501,42 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) void k_pick(SceneView sv, const Gp
   const Hit h = traverse<false>(sv.nodes, sv.tris, r, stack + threadIdx.x);
   const V3 p = org + h.t * dir;
   out[0] = make_float4(p.x, p.y, p.z, __int_as_float(h.tri));
+}
+
+// ---------------------------------------------------------------- arithmetic checks
+// fn 0: rcp_rn(x) against the IEEE division 1.0f/x for every 32-bit pattern x.
+// Mismatches are counted in out[0]; out[1] = the smallest mismatching input bits.
+__global__ __launch_bounds__(256) void k_check_math(int fn, unsigned long long* out) {
+  unsigned long long bad = 0, first = ~0ull;
+  if (fn == 0) {
+    for (unsigned long long i = blockIdx.x * 256ull + threadIdx.x; i < (1ull << 32);
+         i += (unsigned long long)gridDim.x * 256ull) {
+      const float x = __uint_as_float((uint32_t)i);
+      const float got = rcp_rn(x), want = 1.0f / x;
+      if (!(__float_as_uint(got) == __float_as_uint(want) || (got != got && want != want))) {
+        ++bad;
+        first = i < first ? i : first;
+      }
+    }
+  }
+  if (bad) {
+    atomicAdd(&out[0], bad);
+    atomicMin(&out[1], first);
+  }
+}
+
+int check_math(int fn, unsigned long long* host2) {
+  unsigned long long* d = nullptr;
+  if (hipMalloc(&d, 16) != hipSuccess) return -1;
+  const unsigned long long init[2] = {0ull, ~0ull};
+  int rc = 0;
+  if (hipMemcpy(d, init, 16, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+  if (!rc) {
+    hipLaunchKernelGGL(k_check_math, dim3(8192), dim3(256), 0, 0, fn, d);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host2, d, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+  }
+  (void)hipFree(d);
+  return rc;
 }
 
 int trace_profile(unsigned long long* out8, int reset) {

@@ -129,6 +129,8 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
 int trace_profile(unsigned long long* out8, int reset);
+// Arithmetic self-check of the correctly rounded fast reciprocal (rcp_rn): see pathtrace.hip
+int check_math(int fn, unsigned long long* host2);
 // Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (image tile =
 // tileOffset + j * tileStride, j < numTiles) as a slab of numTiles * 256 float4 (rgb float,
 // w = the RGB8 bytes), in tile order j and scan order within the tile; unpack scatters a slab

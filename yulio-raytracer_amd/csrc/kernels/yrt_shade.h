@@ -107,6 +107,7 @@ struct BRDFSet {
 
 struct DG {
   V3 P, Ng, Ns, Tx, Ty;
+  V3 Fx, Fy;    // frame(Ns) = (Fx, Fy, Ns), built once per vertex after Material::shade (dg_frame)
   float s, t;   // st
   float error;
   int material, light, illumMask, shadowMask;
@@ -147,6 +148,24 @@ __device__ __forceinline__ V3 cosine_hemi(float u, float v, V3 N, float& pdf) {
   V3 l = v3(yrt_cosf(phi) * sinTheta, yrt_sinf(phi) * sinTheta, cosTheta);
   pdf = cosTheta * kOneOverPi;
   return mul(frame(N), l);
+}
+
+// frame(Ns) of the shading point, shared by every cosine-weighted / microfacet sample of the
+// vertex (BRDF sampling and the dome light): built once instead of once per sample (each
+// build is two normalizations); same operations, so the same bits as frame(dg.Ns).
+__device__ __forceinline__ void dg_frame(DG& dg) {
+  const L3 F = frame(dg.Ns);
+  dg.Fx = F.vx;
+  dg.Fy = F.vy;
+}
+__device__ __forceinline__ L3 dg_F(const DG& dg) { return l3(dg.Fx, dg.Fy, dg.Ns); }
+// cosineSampleHemisphere(u, v, dg.Ns) with the vertex's prebuilt frame
+__device__ __forceinline__ V3 cosine_hemi_dg(float u, float v, const DG& dg, float& pdf) {
+  const float phi = kTwoPi * u;
+  const float cosTheta = sqrtf(v), sinTheta = sqrtf(1.0f - v);
+  V3 l = v3(yrt_cosf(phi) * sinTheta, yrt_sinf(phi) * sinTheta, cosTheta);
+  pdf = cosTheta * kOneOverPi;
+  return mul(dg_F(dg), l);
 }
 
 // ---------------------------------------------------------------- textures
@@ -352,7 +371,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
   }
   switch (c.kind) {
     case C_LAMBERT: {
-      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return lambert_eval(c.R, dg, wi);
     }
     case C_DIEL_REFL: {
@@ -385,7 +404,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       V3 wo1;
       refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaO1, wo1);
       float pdf1;
-      V3 wi1 = cosine_hemi(sx, sy, dg.Ns, pdf1);
+      V3 wi1 = cosine_hemi_dg(sx, sy, dg, pdf1);
       V3 Fg = lambert_eval(c.R, dg, wi1);
       float cosThetaI1 = dot(wi1, dg.Ns);
       if (cosThetaI1 <= 0.0f) return v3s(0.0f);
@@ -409,7 +428,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float sinPhi = yrt_sinf(phi);
       const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
       const float sinTheta = cos2sin(cosTheta);
-      V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+      V3 wh = mul(dg_F(dg), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
       float whpdf = norm1 * yrt_powf(cosTheta, n);
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
@@ -427,7 +446,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       const float sinPhi = yrt_sinf(phi);
       const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
       const float sinTheta = cos2sin(cosTheta);
-      V3 wh = mul(frame(dg.Ns), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+      V3 wh = mul(dg_F(dg), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
       float whpdf = norm1 * yrt_powf(cosTheta, n);
       wi = reflect2(wo, wh);
       pdf = whpdf * rcpf_(4.0f * fabsf(dot(wo, wh)));
@@ -468,11 +487,11 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return c.R * fresnel_conductor(dot(wo, dg.Ns), mat_eta(mats, c.c), mat_k(mats, c.c));
     }
     case C_MINNAERT: {
-      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return minnaert_eval(c, wo, dg, wi);
     }
     case C_VELVETY: {
-      wi = cosine_hemi(sx, sy, dg.Ns, pdf);
+      wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return velvety_eval(c, wo, dg, wi);
     }
     case C_DIEL_TRANS: {  // dielectric.h:82-89 (the sample's eta is dropped)

@@ -151,6 +151,10 @@ _sig(dev, "yrtGetSceneRefits", i32, vp, vp)
 _sig(dev, "yrtSetRayCapture", i32, vp, i32)
 _sig(dev, "yrtGetCapturedRays", C.c_int64, vp, i32, i32, vp, vp, sz, C.POINTER(C.c_double))
 _sig(dev, "yrtDebugTraceProfile", i32, vp, C.POINTER(C.c_uint64), i32)
+try:  # debug-only entry; absent from older tuning builds selected with YRT_LIB_DIR
+    _sig(dev, "yrtDebugCheckMath", i32, vp, i32, C.POINTER(C.c_uint64))
+except AttributeError:
+    pass
 _sig(dev, "yrtDebugDecodeImage", i32, cstr, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), vp, sz)
 _sig(dev, "yrtDebugSampleTable", i32, i32, i32, i32, i32, i32, cstr, PF, sz)
 
