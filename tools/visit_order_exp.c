@@ -165,9 +165,12 @@ int visit_counts(const void* nodes_, size_t nn, const void* tris_, const float* 
           for (int k = 0; k < 4; ++k) { const int s = (p >> (2 * k)) & 3; t2[k] = t[s]; c2[k] = c[s]; }
           memcpy(t, t2, sizeof t);
           memcpy(c, c2, sizeof c);
-        } else if (mode == 0) {
+        } else if (mode == 0 || mode == 11 || mode == 12) {
+          /* 0: full sort (5 comparators); 11: nearest first only ((0,1),(2,3),(0,2));
+             12: nearest first and farthest last (+ (1,3)) */
           static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
-          for (int m = 0; m < 5; ++m) {
+          const int ncmp = mode == 0 ? 5 : mode == 11 ? 3 : 4;
+          for (int m = 0; m < ncmp; ++m) {
             const int a = net[m][0], b = net[m][1];
             if (t[b] < t[a]) {
               float tt = t[a]; t[a] = t[b]; t[b] = tt;

@@ -300,11 +300,17 @@ __device__ unsigned long long g_traceProfile[8];
 #else
 #define YRT_PROF(i, v) ((void)0)
 #endif
+#ifndef YRT_REFILL_ANY
+#define YRT_REFILL_ANY YRT_REFILL  // refill threshold of the any-hit (shadow) instantiation
+#endif
 #ifndef YRT_TRI_STEP
 #define YRT_TRI_STEP 2  // triangles per lane per leaf step (0 = whole leaf): 2 is +0.7 % over whole leaves
 #endif
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
+#endif
+#ifndef YRT_NODE_BIAS_ANY
+#define YRT_NODE_BIAS_ANY YRT_NODE_BIAS
 #endif
 #ifndef YRT_TRACE_WAVES
 // 6: a scheduling target — the 16 KB LDS stack of a 128-lane block holds the kernels at 5
@@ -339,7 +345,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          int segCap, float4* __restrict__ hitOut,
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
                                                          ShadowFuse sf) {
-  __shared__ int lstack[YRT_LDS_STACK * YRT_TRACE_BLOCK];
+  constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
+  __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   qmap_load(qm, counts, numSegs);
   const unsigned n = qm.pre[YRT_QSEGS];
@@ -368,10 +375,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // The LDS stack is a ring holding the top YRT_LDS_STACK entries; older entries are evicted
   // to global memory on push and restored into the freed slot on pop (both rare). Every pop
   // returns an LDS value, so the hot path stays a ds_read.
-#define YRT_SLOT(i) ((((i) & (YRT_LDS_STACK - 1))) * YRT_TRACE_BLOCK)
+#define YRT_SLOT(i) ((((i) & (kLds - 1))) * YRT_TRACE_BLOCK)
 #define YRT_PUSH(e)                                                               \
   do {                                                                            \
-    if (sp >= YRT_LDS_STACK) spill[(size_t)(sp - YRT_LDS_STACK) * spillStride] = stack[YRT_SLOT(sp)]; \
+    if (sp >= kLds) spill[(size_t)(sp - kLds) * spillStride] = stack[YRT_SLOT(sp)]; \
     stack[YRT_SLOT(sp)] = (e);                                                    \
     sp += 1;                                                                      \
   } while (0)
@@ -382,7 +389,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     } else {                                                                      \
       sp -= 1;                                                                    \
       const unsigned e_ = (unsigned)stack[YRT_SLOT(sp)];                          \
-      if (sp >= YRT_LDS_STACK) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - YRT_LDS_STACK) * spillStride]; \
+      if (sp >= kLds) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - kLds) * spillStride]; \
       curIdx = (int)(e_ >> 5);                                                    \
       curCnt = (int)(e_ & 31u);                                                   \
     }                                                                             \
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     const int nIdle = __popcll(idle);
     YRT_PROF(0, 1);
     YRT_PROF(1, 64 - nIdle);
-    if (nIdle >= YRT_REFILL) {
+    if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
       if (next < end) {
         if (!has) {
           const unsigned li = next + (unsigned)__popcll(idle & ltMask);
@@ -467,7 +474,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     // another is parked, or only a parked leaf is left); otherwise a leaf step
     const int nNode = __popcll(__ballot(has && curCnt == 0));
     const int nBlocked = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
-    if (nNode * 4 > nBlocked * YRT_NODE_BIAS) {
+    if (nNode * 4 > nBlocked * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS)) {
      // consecutive node steps without the retire/refill block in between (+1.5 % on C3)
      while (true) {
       YRT_PROF(2, 1);
@@ -484,7 +491,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         else sort3_far(t, c);
         const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
 #define YRT_HIT(x) (ANY ? (x) > MISS : (x) < MISS)
-        if (sp + 3 <= YRT_LDS_STACK) {
+        if (sp + 3 <= kLds) {
           // all three candidates fit in free ring slots: store unconditionally, advance sp
           // only past the hit ones (a store of a missed child lands on a free slot);
           // shadow rays -4..9 %, closest neutral (profiles/r01)
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       }
       const int nNode2 = __popcll(__ballot(has && curCnt == 0));
       const int nBlocked2 = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
-      if (!(nNode2 * 4 > nBlocked2 * YRT_NODE_BIAS)) break;
+      if (!(nNode2 * 4 > nBlocked2 * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS))) break;
      }
     } else {
       // leaf step: the parked leaf, or else the current entry when it is a leaf

@@ -38,7 +38,7 @@ struct SceneView {
 #ifndef YRT_TRACE_GRID
 #define YRT_TRACE_GRID 16384
 #endif
-#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * YRT_TRACE_BLOCK * (YRT_STACK_DEPTH - YRT_LDS_STACK))
+#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * YRT_TRACE_BLOCK * (YRT_STACK_DEPTH - YRT_LDS_STACK_MIN))
 
 struct FrameView {
   const GpuRenderParams* rp;   // device copy

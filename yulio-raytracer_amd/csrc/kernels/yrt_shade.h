@@ -14,8 +14,8 @@
 //   textures        textures/{Bilinear,nearestneighbor}.h, texel decode
 //                   common/math/color_scalar.h:47 (byte * one_over_255)
 // Omitted reference features (no BASELINE config reaches them): motion blur, metallic-paint
-// glitter, the Beckmann distributions (no material instantiates them), the backplate image;
-// DESIGN.md lists them.
+// glitter, the Beckmann distributions (no material instantiates them); DESIGN.md §7 lists them.
+// The backplate image is read in k_shade (pathtrace.hip) for camera-ray misses.
 #pragma once
 
 #include "../common/yrt_gpu_types.h"

@@ -29,10 +29,19 @@
 #define YRT_LDS_STACK 32     // top entries kept in LDS; deeper ones spill (power of two)
 #endif
 static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
+#ifndef YRT_LDS_STACK_ANY
+#define YRT_LDS_STACK_ANY YRT_LDS_STACK  // LDS ring of the any-hit (shadow) instantiation
+#endif
+static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
+#define YRT_LDS_STACK_MIN (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
 #ifndef YRT_TRACE_BLOCK
 // one wave per block (8 KB of LDS stack): +1.0 % on C3 over 128-lane blocks once the trace code
 // was scheduled for a 6-wave target (profiles/r01/variants_r01.txt)
 #define YRT_TRACE_BLOCK 64
+#endif
+
+#ifndef YRT_ASM_MINMAX
+#define YRT_ASM_MINMAX 1  // +1.5 % on C3 (shadow trace 5.84 -> 5.38 ms/launch), profiles/r02/trace_variants_r02.txt
 #endif
 
 namespace yrt {
@@ -140,6 +149,22 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
   const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz, oz2), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz, oz2);
 #undef YRT_SLAB
   const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
+#if YRT_ASM_MINMAX
+  // v_max/v_min written out: fmaxf/fminf on the loop-carried tnear / tfar make the compiler
+  // re-quiet (canonicalize) them with an extra v_max every node step (IEEE mode). A signalling
+  // NaN never reaches here (ray records are computed values), and the hardware min/max give
+  // the same result as fmaxf/fminf for every other input.
+#define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                            \
+  do {                                                                                      \
+    float nn, ff, a_, b_;                                                                   \
+    asm("v_max_f32 %0, %1, %2" : "=v"(a_) : "v"(NZ), "v"(r.tnear));                         \
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(nn) : "v"(NX), "v"(NY), "v"(a_));                \
+    asm("v_min_f32 %0, %1, %2" : "=v"(b_) : "v"(FZ), "v"(tmax));                            \
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(ff) : "v"(FX), "v"(FY), "v"(b_));                \
+    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;                  \
+    c[k] = (CH);                                                                            \
+  } while (0)
+#else
 #define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                    \
   do {                                                                              \
     const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                      \
@@ -147,6 +172,7 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
     t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;          \
     c[k] = (CH);                                                                    \
   } while (0)
+#endif
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
   YRT_CHILD(1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y, ch.y);
   YRT_CHILD(2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x, ch.z);
@@ -155,6 +181,8 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
 }
 
 // Sorts the four (t, child) pairs by t ascending (5-comparator network, stable for equal t).
+// (A 3-comparator nearest-first order saves 10 VALU per node step but visits 1.4 % more nodes:
+// -0.6 % on C3, profiles/r02/trace_variants_r02.txt.)
 __device__ __forceinline__ void sort4(float t[4], int c[4]) {
 #define YRT_CSWAP(a, b)                          \
   do {                                           \
