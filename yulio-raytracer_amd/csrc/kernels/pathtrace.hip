@@ -691,16 +691,18 @@ template <unsigned MM>
 __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, int matId, int medium, DG& dg,
                                                BRDFSet& bs) {
   bs.n = 0;
-  if (!(MM & mat_bit(m.type))) return;
+  // each case is compiled only when the instantiation's material set MM holds its type
   const float idBits = __int_as_float(matId);
   switch (m.type) {
     case MAT_PLASTIC:
+      if constexpr (!(MM & mat_bit(MAT_PLASTIC))) break;
       // p: pigment[0..2], eta[3], roughness[4], rcpRoughness[5], layer etait[6], etati[7], eta_[8]
       add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[6], m.p[7]);
       if (m.p[4] == 0.0f) add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[8], 1.0f);
       else add_comp(bs, C_MICROFACET, BT_GLOSSY_REFLECTION, v3s(1.f), 1.0f, m.p[3], m.p[5]);
       break;
     case MAT_DIELECTRIC:
+      if constexpr (!(MM & mat_bit(MAT_DIELECTRIC))) break;
       // outside -> inside when the ray travels in the outside medium (dielectric.h:42-52)
       if (medium == m.media[0]) {
         add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[8], 1.0f);
@@ -711,14 +713,17 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       }
       break;
     case MAT_MIRROR:
+      if constexpr (!(MM & mat_bit(MAT_MIRROR))) break;
       add_comp(bs, C_REFLECTION, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
       break;
     case MAT_METAL:
+      if constexpr (!(MM & mat_bit(MAT_METAL))) break;
       // p: R[0..2], eta[3..5], k[6..8], roughness[9], rcpRoughness[10]
       if (m.p[9] == 0.0f) add_comp(bs, C_CONDUCTOR, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), 0.f, 0.f, idBits);
       else add_comp(bs, C_MICRO_COND, BT_GLOSSY_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[10], 0.f, idBits);
       break;
     case MAT_BRUSHED_METAL:
+      if constexpr (!(MM & mat_bit(MAT_BRUSHED_METAL))) break;
       // p: R[0..2], eta[3..5], k[6..8], roughnessX[9], roughnessY[10], rcp[11], rcp[12]
       if (m.p[9] == 0.0f || m.p[10] == 0.0f)
         add_comp(bs, C_CONDUCTOR, BT_SPECULAR_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), 0.f, 0.f, idBits);
@@ -726,13 +731,16 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
         add_comp(bs, C_MICRO_ANISO, BT_GLOSSY_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[11], m.p[12], idBits);
       break;
     case MAT_VELVET:
+      if constexpr (!(MM & mat_bit(MAT_VELVET))) break;
       add_comp(bs, C_MINNAERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[3]);
       add_comp(bs, C_VELVETY, BT_DIFFUSE_REFLECTION, v3(m.p[4], m.p[5], m.p[6]), m.p[7]);
       break;
     case MAT_MATTE:
+      if constexpr (!(MM & mat_bit(MAT_MATTE))) break;
       add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]));
       break;
     case MAT_MATTE_TEXTURED:
+      if constexpr (!(MM & mat_bit(MAT_MATTE_TEXTURED))) break;
       if (m.tex[0] >= 0) {
         float c[4];
         tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
@@ -740,11 +748,13 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       }
       break;
     case MAT_METALLIC_PAINT:
+      if constexpr (!(MM & mat_bit(MAT_METALLIC_PAINT))) break;
       // p: shadeColor[0..2], eta[3], reflection eta_ [4], layer etait [5], etati [6]
       add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[4], 1.0f);
       add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[5], m.p[6]);
       break;
     case MAT_OBJ: {
+      if constexpr (!(MM & mat_bit(MAT_OBJ))) break;
       // p: d[0], Kd[1..3], Ks[4..6], Ns[7]; tex: map_d, map_Kd, map_Ks, map_Ns, map_Bump
       float c[4];
       if (m.tex[4] >= 0) {
@@ -778,6 +788,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       break;
     }
     case MAT_UBER: {
+      if constexpr (!(MM & mat_bit(MAT_UBER))) break;
       // p: diffuse[0..2], s0[3..4], ds[5..6], eta[7], roughness[8], reflectivity[9],
       //    rcpRoughness[10], eta_ = 1*rcp(eta) [11]
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
@@ -795,6 +806,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       break;
     }
     case MAT_THIN_DIELECTRIC: {
+      if constexpr (!(MM & mat_bit(MAT_THIN_DIELECTRIC))) break;
       // p: transmission[0..2], s0[3..4], ds[5..6], eta[7], thickness[8], transparency[9], eta_[10]
       add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[10], 1.0f);
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
@@ -849,9 +861,11 @@ __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V
   return r;
 }
 
-// LM: the light types (bit LIGHT_x) an instantiation handles; the shade kernel uses every type
-// (specializing per scene light set measured neutral-to-worse on C3).
+// LM: the light types (bit LIGHT_x) an instantiation handles: bits 16.. of the shade kernel's
+// instantiation mask (light_bit), which the launcher picks as a superset of the scene's lights.
 constexpr unsigned kAllLights = 0x7Fu;
+template <unsigned MM>
+constexpr unsigned lights_of() { return (MM >> 16) & kAllLights; }
 template <unsigned LM>
 __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
   if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
@@ -923,13 +937,18 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
   return v3s(0.f);
 }
 
-// Occupancy target for k_shade: 3 waves/SIMD caps it at 168 VGPRs with a few bytes of spill
-// (unconstrained it takes 183 VGPRs = 2 waves/SIMD).
+// Occupancy target for k_shade. With the material / component / light cases pruned per
+// instantiation (if constexpr), the Uber kernel needs 125 VGPRs: 4 waves/SIMD. Same box, C3:
+// 3 waves 420.4, 4 waves 419.5, 5 waves 436.9 ms/frame (profiles/r02/shade_prune_r02.txt).
 #ifndef YRT_SHADE_WAVES
-#define YRT_SHADE_WAVES 3
+#define YRT_SHADE_WAVES 4
+#endif
+#ifndef YRT_SHADE_WAVES_ALL
+#define YRT_SHADE_WAVES_ALL 2  // the generic all-types instantiation (rare scenes): no spills at 2
 #endif
 template <unsigned MM>
-__global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
+__global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
+    MM == (YRT_ALL_MATS | YRT_ALL_LIGHTS) ? YRT_SHADE_WAVES_ALL : YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
 #ifdef YRT_SHADE_PROF
   // shader-clock cycles per phase (wave-uniform points only), summed over the waves
@@ -1027,7 +1046,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         } else if (!ignoreVL) {
           for (int j = 0; j < sv.numEnvLights; ++j) {
             if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
-            L = L + thr * env_Le<kAllLights>(sv, sv.lights[sv.envLights[j]], wo);
+            L = L + thr * env_Le<lights_of<MM>()>(sv, sv.lights[sv.envLights[j]], wo);
           }
         }
       }
@@ -1152,7 +1171,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(YRT_S
         } else {
           const float lsx = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID, rec);
           const float lsy = samp(fv, 5 + rp.dim1D + 2 * rp.lightSampleID + 1, rec);
-          Ls = light_sample<kAllLights>(lt, dg, lsx, lsy, wi, pdf);
+          Ls = light_sample<lights_of<MM>()>(lt, dg, lsx, lsy, wi, pdf);
         }
       }
       SPROF_FINE(3);  // Light::sample

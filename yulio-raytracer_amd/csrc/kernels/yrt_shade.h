@@ -238,6 +238,10 @@ __device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures,
 }
 
 // ---------------------------------------------------------------- BRDF components
+// Component-set guards (CM = the kernel instantiation's component bitmask)
+#define YRT_IF(K) if constexpr ((CM & comp_bit(K)) != 0u)
+#define YRT_IF_NOT(K) if constexpr ((CM & comp_bit(K)) == 0u)
+
 __device__ __forceinline__ V3 lambert_eval(V3 R, const DG& dg, V3 wi) {
   return R * kOneOverPi * clampf(dot(wi, dg.Ns));
 }
@@ -345,48 +349,49 @@ __device__ __forceinline__ V3 specular_eval(const Comp& c, V3 wo, const DG& dg, 
 template <unsigned CM>
 __device__ __forceinline__ V3 comp_eval(const Comp c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
                                         V3 wi) {
-  if (!(CM & comp_bit(c.kind))) return v3s(0.0f);
+  // YRT_IF(K): the case is compiled only when the component set CM can hold kind K (a runtime
+  // bit test does not let the compiler drop switch cases; these constexpr guards do)
   switch (c.kind) {
-    case C_LAMBERT: return lambert_eval(c.R, dg, wi);
-    case C_DIEL_LAYER_LAMB: return layer_eval(c, wo, dg, wi);
-    case C_MICROFACET:
-    case C_MICRO_COND:
-    case C_MICRO_ANISO: return microfacet_eval<CM>(c, mats, wo, dg, wi);
-    case C_SPECULAR: return specular_eval(c, wo, dg, wi);
-    case C_REFLECTION: return c.R;  // Reflection::eval (reflection.h:16-18)
-    case C_MINNAERT: return minnaert_eval(c, wo, dg, wi);
-    case C_VELVETY: return velvety_eval(c, wo, dg, wi);
-    default: return v3s(0.0f);
+    case C_LAMBERT: YRT_IF(C_LAMBERT) return lambert_eval(c.R, dg, wi); break;
+    case C_DIEL_LAYER_LAMB: YRT_IF(C_DIEL_LAYER_LAMB) return layer_eval(c, wo, dg, wi); break;
+    case C_MICROFACET: YRT_IF(C_MICROFACET) return microfacet_eval<CM>(c, mats, wo, dg, wi); break;
+    case C_MICRO_COND: YRT_IF(C_MICRO_COND) return microfacet_eval<CM>(c, mats, wo, dg, wi); break;
+    case C_MICRO_ANISO: YRT_IF(C_MICRO_ANISO) return microfacet_eval<CM>(c, mats, wo, dg, wi); break;
+    case C_SPECULAR: YRT_IF(C_SPECULAR) return specular_eval(c, wo, dg, wi); break;
+    case C_REFLECTION: YRT_IF(C_REFLECTION) return c.R; break;  // Reflection::eval (reflection.h:16-18)
+    case C_MINNAERT: YRT_IF(C_MINNAERT) return minnaert_eval(c, wo, dg, wi); break;
+    case C_VELVETY: YRT_IF(C_VELVETY) return velvety_eval(c, wo, dg, wi); break;
+    default: break;
   }
+  return v3s(0.0f);
 }
 
 // BRDF::sample of one component; returns color, sets wi/pdf.
 template <unsigned CM>
 __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
                                           float sx, float sy, V3& wi, float& pdf) {
-  if (!(CM & comp_bit(c.kind))) {
-    pdf = 0.0f;
-    wi = v3s(0.0f);
-    return v3s(0.0f);
-  }
   switch (c.kind) {
     case C_LAMBERT: {
+      YRT_IF_NOT(C_LAMBERT) break;
       wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return lambert_eval(c.R, dg, wi);
     }
     case C_DIEL_REFL: {
+      YRT_IF_NOT(C_DIEL_REFL) break;
       const float cosThetaO = clampf(dot(wo, dg.Ns));
       wi = reflect3(wo, dg.Ns, cosThetaO);
       pdf = 1.0f;
       return c.b * v3s(fresnel2(cosThetaO, c.a, nullptr));
     }
     case C_CONST_DIEL_TRANS: {
+      YRT_IF_NOT(C_CONST_DIEL_TRANS) break;
       wi = -wo;
       pdf = 1.0f;
       const float cosTheta = clampf(dot(wo, dg.Ns));
       return cosTheta <= 0.0f ? v3s(0.0f) : c.R;
     }
     case C_THIN_DIEL_TRANS: {
+      YRT_IF_NOT(C_THIN_DIEL_TRANS) break;
       wi = -wo;
       pdf = 1.0f;
       const float cosTheta = clampf(dot(wo, dg.Ns));
@@ -397,6 +402,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return v3(yrt_expf(la.x), yrt_expf(la.y), yrt_expf(la.z)) * (1.f - fresnel2(cosTheta, c.a, &cosThetaT));
     }
     case C_DIEL_LAYER_LAMB: {
+      YRT_IF_NOT(C_DIEL_LAYER_LAMB) break;
       pdf = 0.0f;
       float cosThetaO = dot(wo, dg.Ns);
       if (cosThetaO <= 0.0f) return v3s(0.0f);
@@ -419,6 +425,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
     }
     case C_MICROFACET: {
+      YRT_IF_NOT(C_MICROFACET) break;
       pdf = 0.0f;
       if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
       const float n = c.c;
@@ -436,6 +443,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_MICRO_COND: {
+      YRT_IF_NOT(C_MICRO_COND) break;
       // Microfacet::sample (microfacet.h:43-50) with PowerCosineDistribution::sample
       pdf = 0.0f;
       if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
@@ -454,6 +462,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_MICRO_ANISO: {
+      YRT_IF_NOT(C_MICRO_ANISO) break;
       // AnisotropicPowerCosineDistribution::sample (:57-73)
       pdf = 0.0f;
       if (dot(wo, dg.Ns) <= 0.0f) return v3s(0.0f);
@@ -477,35 +486,42 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       return microfacet_eval<CM>(c, mats, wo, dg, wi);
     }
     case C_REFLECTION: {  // reflection.h:19-22
+      YRT_IF_NOT(C_REFLECTION) break;
       wi = reflect2(wo, dg.Ns);
       pdf = 1.0f;
       return c.R;
     }
     case C_CONDUCTOR: {  // conductor.h:21-24
+      YRT_IF_NOT(C_CONDUCTOR) break;
       wi = reflect2(wo, dg.Ns);
       pdf = 1.0f;
       return c.R * fresnel_conductor(dot(wo, dg.Ns), mat_eta(mats, c.c), mat_k(mats, c.c));
     }
     case C_MINNAERT: {
+      YRT_IF_NOT(C_MINNAERT) break;
       wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return minnaert_eval(c, wo, dg, wi);
     }
     case C_VELVETY: {
+      YRT_IF_NOT(C_VELVETY) break;
       wi = cosine_hemi_dg(sx, sy, dg, pdf);
       return velvety_eval(c, wo, dg, wi);
     }
     case C_DIEL_TRANS: {  // dielectric.h:82-89 (the sample's eta is dropped)
+      YRT_IF_NOT(C_DIEL_TRANS) break;
       const float cosThetaO = clampf(dot(wo, dg.Ns));
       float cosThetaI;
       pdf = refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaI, wi);
       return v3s(1.0f - fresnel3(cosThetaO, cosThetaI, c.a));
     }
     case C_TRANSMISSION: {
+      YRT_IF_NOT(C_TRANSMISSION) break;
       wi = -wo;
       pdf = 1.0f;
       return c.R;
     }
     case C_SPECULAR: {
+      YRT_IF_NOT(C_SPECULAR) break;
       // powerCosineSampleHemisphere(s.x, s.y, reflect(wo, Ns), exp) (shapesampler.h:104-121)
       const float e = c.a;
       const float phi = kTwoPi * sx;
@@ -518,6 +534,7 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
     }
   }
   pdf = 0.0f;
+  wi = v3s(0.0f);
   return v3s(0.0f);
 }
 
