@@ -56,7 +56,7 @@ struct Hit {
 #define YRT_BOX_ROBUST 1.00000036f
 
 __device__ __forceinline__ float safe_inv(float d) {
-  return 1.0f / (fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d));
+  return rcp_rn(fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d));  // correctly rounded: the bits of 1.0f / x
 }
 
 struct RayPre {
