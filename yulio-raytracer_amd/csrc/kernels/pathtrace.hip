@@ -974,6 +974,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
 #endif
   const GpuRenderParams& rp = *fv.rp;
   __shared__ QMap qm;
+  __shared__ float sstash[7 * YRT_MAX_COMPS * YRT_BLOCK];  // set_sample candidates, [slot][lane]
   qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
   const int n = (int)qm.pre[YRT_QSEGS];
   const int cur = depthLevel & 1;
@@ -1111,7 +1112,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     float spdf = 0.f;
     uint32_t stype = 0;
     V3 sc = v3s(0.f);
-    if (doSample) sc = set_sample<comps_of(MM)>(bs, sv.materials, wo, dg, sx, sy, ss, nwi, spdf, stype);
+    if (doSample)
+      sc = set_sample<comps_of(MM)>(bs, sv.materials, wo, dg, sx, sy, ss, nwi, spdf, stype, sstash + threadIdx.x);
     SPROF_FINE(1);  // CompositedBRDF::sample
     if (doSample) {
       {
