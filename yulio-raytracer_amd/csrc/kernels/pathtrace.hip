@@ -296,7 +296,10 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 __device__ unsigned long long g_traceProfile[8];
 #endif
 #ifdef YRT_PROFILE
-#define YRT_PROF(i, v) prof[i] += (unsigned long long)(v)
+#ifndef YRT_PROFILE_ANY
+#define YRT_PROFILE_ANY 0  // which instantiation counts: 0 closest hit, 1 any hit
+#endif
+#define YRT_PROF(i, v) (ANY == (YRT_PROFILE_ANY != 0) ? (void)(prof[i] += (unsigned long long)(v)) : (void)0)
 #else
 #define YRT_PROF(i, v) ((void)0)
 #endif
