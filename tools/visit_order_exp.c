@@ -57,11 +57,51 @@ static uint8_t* octant_orders(const DNode* nodes, size_t nn) {
   return ord;
 }
 
+/* One canonical child order per node (children by box centre along one axis, stored that way)
+ * and its reversal when the ray's direction on that axis is negative: 13 = the axis of the
+ * largest spread of the child centres, 14 = the axis of the node's largest extent. Per node:
+ * order bits 0-7, axis bits 8-9. */
+static uint16_t* axis_orders(const DNode* nodes, size_t nn, int variant) {
+  uint16_t* ord = (uint16_t*)malloc(nn * 2);
+  for (size_t i = 0; i < nn; ++i) {
+    const DNode* n = &nodes[i];
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 4; ++k) {
+      if (n->child[k] == -1) continue;
+      const float lo[3] = {n->lox[k], n->loy[k], n->loz[k]}, hi[3] = {n->hix[k], n->hiy[k], n->hiz[k]};
+      for (int a = 0; a < 3; ++a) {
+        const float c = lo[a] + hi[a];
+        cmin[a] = fminf(cmin[a], c); cmax[a] = fmaxf(cmax[a], c);
+        bmin[a] = fminf(bmin[a], lo[a]); bmax[a] = fmaxf(bmax[a], hi[a]);
+      }
+    }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a) {
+      const float ea = variant == 13 ? cmax[a] - cmin[a] : bmax[a] - bmin[a];
+      const float e0 = variant == 13 ? cmax[ax] - cmin[ax] : bmax[ax] - bmin[ax];
+      if (ea > e0) ax = a;
+    }
+    float key[4];
+    int s[4] = {0, 1, 2, 3};
+    for (int k = 0; k < 4; ++k) {
+      const float lo[3] = {n->lox[k], n->loy[k], n->loz[k]}, hi[3] = {n->hix[k], n->hiy[k], n->hiz[k]};
+      key[k] = n->child[k] == -1 ? INFINITY : lo[ax] + hi[ax];
+    }
+    for (int a = 0; a < 4; ++a)
+      for (int b = a + 1; b < 4; ++b)
+        if (key[s[b]] < key[s[a]]) { int t = s[a]; s[a] = s[b]; s[b] = t; }
+    ord[i] = (uint16_t)(s[0] | s[1] << 2 | s[2] << 4 | s[3] << 6 | ax << 8);
+  }
+  return ord;
+}
+
 int visit_counts(const void* nodes_, size_t nn, const void* tris_, const float* org4, const float* dir4, int n,
                  int anyHit, int mode, double* out3) {
   const DNode* nodes = (const DNode*)nodes_;
   const DTri* tris = (const DTri*)tris_;
   uint8_t* ord = (mode == 1 || mode == 6 || mode == 9) ? octant_orders(nodes, nn) : NULL;
+  uint16_t* aord = (mode == 13 || mode == 14) ? axis_orders(nodes, nn, mode) : NULL;
   double nv = 0, tv = 0, pushes = 0;
   for (int i = 0; i < n; ++i) {
     const float o[3] = {org4[4 * i], org4[4 * i + 1], org4[4 * i + 2]};
@@ -195,6 +235,18 @@ int visit_counts(const void* nodes_, size_t nn, const void* tris_, const float* 
           for (int k = 0; k < 4; ++k) { t2[k] = t[s4[k]]; c2[k] = c[s4[k]]; }
           memcpy(t, t2, sizeof t);
           memcpy(c, c2, sizeof c);
+        } else if (mode == 13 || mode == 14) {
+          const uint16_t p = aord[ni];
+          const int ax = p >> 8;
+          const int rev = d[ax] < 0.f;
+          float t2[4];
+          int c2[4];
+          for (int k = 0; k < 4; ++k) {
+            const int s = (p >> (2 * (rev ? 3 - k : k))) & 3;
+            t2[k] = t[s]; c2[k] = c[s];
+          }
+          memcpy(t, t2, sizeof t);
+          memcpy(c, c2, sizeof c);
         } else if (mode == 1) {
           const uint8_t p = ord[(size_t)ni * 8 + oct];
           float t2[4];
@@ -229,6 +281,7 @@ int visit_counts(const void* nodes_, size_t nn, const void* tris_, const float* 
     }
   }
   free(ord);
+  free(aord);
   out3[0] = nv / n;
   out3[1] = tv / n;
   out3[2] = pushes / n;

@@ -18,7 +18,7 @@ lib.visit_counts.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c
 z = np.load(sys.argv[1] if len(sys.argv) > 1 else ROOT / "gpurun_out" / "rays_c3.npz")
 nodes, tris = z["nodes"], z["tris"]
 nn = len(nodes) // 128
-modes = {0: "distance", 1: "octant", 2: "slot", 3: "area-desc", 4: "area-asc", 5: "far-first", 6: "oct-rev", 7: "far1+slot", 8: "far-net3", 9: "octfar1", 10: "bound", 11: "near-net3", 12: "near-net4"}
+modes = {0: "distance", 1: "octant", 2: "slot", 3: "area-desc", 4: "area-asc", 5: "far-first", 6: "oct-rev", 7: "far1+slot", 8: "far-net3", 9: "octfar1", 10: "bound", 11: "near-net3", 12: "near-net4", 13: "axis-cent", 14: "axis-box"}
 for kind in ("c", "s"):
     tot = {m: np.zeros(3) for m in modes}
     wsum = 0.0
