@@ -45,8 +45,11 @@ __device__ __forceinline__ unsigned wave_reserve(unsigned* counter, unsigned k) 
   return base + incl - k;
 }
 
+// Ballot of a bool (the builtin on the i1 lane mask; HIP's __ballot takes an int).
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ unsigned wave_append(unsigned* counter, bool pred, bool& got) {
-  const unsigned long long mask = __ballot(pred);
+  const unsigned long long mask = ballot(pred);
   got = pred;
   if (mask == 0) return 0;
   const int lane = lane_id();
@@ -303,6 +306,7 @@ __device__ unsigned long long g_traceProfile[8];
 #else
 #define YRT_PROF(i, v) ((void)0)
 #endif
+
 #ifndef YRT_REFILL_ANY
 #define YRT_REFILL_ANY YRT_REFILL  // refill threshold of the any-hit (shadow) instantiation
 #endif
@@ -379,6 +383,11 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // to global memory on push and restored into the freed slot on pop (both rare). Every pop
   // returns an LDS value, so the hot path stays a ds_read.
 #define YRT_SLOT(i) ((((i) & (kLds - 1))) * YRT_TRACE_BLOCK)
+#define YRT_POP_READ(e_)                                                          \
+  do {                                                                            \
+    e_ = (unsigned)stack[YRT_SLOT(sp)];                                           \
+    if (sp >= kLds) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - kLds) * spillStride]; \
+  } while (0)
 #define YRT_PUSH(e)                                                               \
   do {                                                                            \
     if (sp >= kLds) spill[(size_t)(sp - kLds) * spillStride] = stack[YRT_SLOT(sp)]; \
@@ -391,8 +400,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       curCnt = -1;                                                                \
     } else {                                                                      \
       sp -= 1;                                                                    \
-      const unsigned e_ = (unsigned)stack[YRT_SLOT(sp)];                          \
-      if (sp >= kLds) stack[YRT_SLOT(sp)] = spill[(size_t)(sp - kLds) * spillStride]; \
+      unsigned e_;                                                                \
+      YRT_POP_READ(e_);                                                           \
       curIdx = (int)(e_ >> 5);                                                    \
       curCnt = (int)(e_ & 31u);                                                   \
     }                                                                             \
@@ -403,6 +412,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   Hit best;
   best.t = best.u = best.v = 0.f;
   best.tri = -1;
+  // closest hit: the accepted triangle's undivided barycentrics (U, V) and |den| are kept, and
+  // u = U/|den|, v = V/|den| are divided once, when the finished query is stored at the next
+  // refill (or at the wave's end), instead of at every accepted hit; q = -1: nothing to store
+  float bestDen = 1.f;
+  q = -1;
+#define YRT_STORE_HIT()                                                                              \
+  do {                                                                                               \
+    hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));   \
+    q = -1;                                                                                          \
+  } while (0)
   const unsigned long long ltMask = (1ull << lane) - 1ull;
 
 #ifdef YRT_PROFILE
@@ -412,16 +431,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     // retire lanes whose traversal is complete
     if (has && curCnt < 0 && pendCnt == 0) {
       if (ANY) shadow_done(sf, occOut, q, false);
-      else hitOut[q] = make_float4(best.t, best.u, best.v, __int_as_float(best.tri));
       has = false;
     }
-    const unsigned long long idle = __ballot(!has);
+    const unsigned long long idle = ballot(!has);
     const int nIdle = __popcll(idle);
     YRT_PROF(0, 1);
     YRT_PROF(1, 64 - nIdle);
     if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
       if (next < end) {
         if (!has) {
+          if (!ANY && q >= 0) YRT_STORE_HIT();
           const unsigned li = next + (unsigned)__popcll(idle & ltMask);
           if (li < end) {
             q = qmap_phys(qm, segCap, li);
@@ -438,6 +457,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             best.t = rd.w;
             best.u = best.v = 0.f;
             best.tri = -1;
+            bestDen = 1.f;
             sp = 0;
             curIdx = 0;
             curCnt = 0;
@@ -446,12 +466,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             has = rd.w >= ro.w;
             if (!has) {
               if (ANY) shadow_done(sf, occOut, q, false);
-              else hitOut[q] = make_float4(best.t, 0.f, 0.f, __int_as_float(-1));
             }
           }
         }
         next += (unsigned)nIdle;
       } else if (nIdle == 64) {
+        if (!ANY && q >= 0) YRT_STORE_HIT();
 #ifdef YRT_PROFILE
         if (lane == 0)
           for (int k = 0; k < 8; ++k) atomicAdd(&g_traceProfile[k], prof[k]);
@@ -475,13 +495,20 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     // finish rejoin at once instead of idling until the wave's phase ends.
     // node step when more lanes can descend than are blocked on a leaf (cur is a leaf while
     // another is parked, or only a parked leaf is left); otherwise a leaf step
-    const int nNode = __popcll(__ballot(has && curCnt == 0));
-    const int nBlocked = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
+    // lane masks of plain comparisons (one v_cmp each) combined on the scalar unit: a ballot of
+    // has && ... re-materializes the predicate per ballot (8 -> 3 VALU per node-step check,
+    // closest-hit trace -2.1 % on C3, profiles/r02/trace_variants_r02.txt); has does not change
+    // inside the node loop, so its mask is taken once here
+    const unsigned long long hasB = ballot(has);
+#define YRT_NNODE() __popcll(ballot(curCnt == 0) & hasB)
+#define YRT_NBLOCKED() __popcll(ballot(max(pendCnt, curCnt) > 0) & ~ballot(curCnt == 0) & hasB)
+    const int nNode = YRT_NNODE();
+    const int nBlocked = YRT_NBLOCKED();
     if (nNode * 4 > nBlocked * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS)) {
      // consecutive node steps without the retire/refill block in between (+1.5 % on C3)
      while (true) {
       YRT_PROF(2, 1);
-      YRT_PROF(3, __popcll(__ballot(has && curCnt == 0)));
+      YRT_PROF(3, __popcll(ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
         float t[4];
         int c[4];
@@ -521,8 +548,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
       }
-      const int nNode2 = __popcll(__ballot(has && curCnt == 0));
-      const int nBlocked2 = __popcll(__ballot(has && curCnt != 0 && (pendCnt > 0 || curCnt > 0)));
+      const int nNode2 = YRT_NNODE();
+      const int nBlocked2 = YRT_NBLOCKED();
       if (!(nNode2 * 4 > nBlocked2 * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS))) break;
      }
     } else {
@@ -564,7 +591,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             ok = tri_test_t(tr, r, r.tfar, t2, U2, V2, a2);
           }
           if (ok) {
-            best.t = t; best.u = U / absDen; best.v = V / absDen; best.tri = gid;
+            best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
           }
         }
       }
