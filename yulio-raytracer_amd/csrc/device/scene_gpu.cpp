@@ -31,6 +31,7 @@ static void bind_view(GpuScene& S) {
   v.textures = S.textures.as<GpuTexture>();
   v.images = S.images.as<GpuImage>();
   v.texels = S.texels.as<uint8_t>();
+  v.texQuads = S.texQuads.as<uint8_t>();
   v.lights = S.lights.as<GpuLight>();
   v.envLights = S.envLights.as<int>();
   v.media = S.media.as<float4>();
@@ -253,6 +254,29 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->textures.upload(textures);
   S->images.upload(images);
   S->texels.upload(texels);
+  {
+    // bilinear footprints of the 8-bit images (kernels/yrt_shade.h tex_get): record i of an image
+    // holds the 4-byte texels i, i+1, i+W, i+W+1 — the bytes the four row-major fetches read —
+    // at 4x the texel's byte offset; float images keep the row-major pool only
+    std::vector<uint32_t> quads(texels.size(), 0u);
+    auto word = [&](size_t b) -> uint32_t {
+      uint32_t w = 0;
+      if (b + 4 <= texels.size()) memcpy(&w, &texels[b], 4);
+      return w;
+    };
+    for (const GpuImage& g : images) {
+      if (g.format == IMG_RGBAF32) continue;
+      const size_t n = (size_t)g.width * g.height, W = (size_t)g.width;
+      for (size_t i = 0; i < n; ++i) {
+        const size_t b = (size_t)g.offset + 4 * i, q = b;  // uint32 index of the record = byte offset
+        quads[q + 0] = word(b);
+        quads[q + 1] = word(b + 4);
+        quads[q + 2] = word(b + 4 * W);
+        quads[q + 3] = word(b + 4 * W + 4);
+      }
+    }
+    S->texQuads.upload(quads);
+  }
   S->lights.upload(lights);
   S->envLights.upload(envLights);
   S->media.upload(media);
@@ -329,6 +353,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   copy(R->textures, src.textures);
   copy(R->images, src.images);
   copy(R->texels, src.texels);
+  copy(R->texQuads, src.texQuads);
   copy(R->lights, src.lights);
   copy(R->envLights, src.envLights);
   copy(R->media, src.media);

@@ -58,7 +58,7 @@ struct GpuScene {
     static std::atomic<uint64_t> n{1};
     return n++;
   }
-  DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels,
+  DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
       lights, envLights, hdriDist, media;
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)

@@ -773,7 +773,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       if constexpr (!(MM & mat_bit(MAT_MATTE_TEXTURED))) break;
       if (m.tex[0] >= 0) {
         float c[4];
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
         add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(c[0], c[1], c[2]));
       }
       break;
@@ -788,30 +788,30 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       // p: d[0], Kd[1..3], Ks[4..6], Ns[7]; tex: map_d, map_Kd, map_Ks, map_Ns, map_Bump
       float c[4];
       if (m.tex[4] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[4], dg.s, dg.t, c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[4], dg.s, dg.t, c);
         const V3 b = v3(2.0f * c[0] - 1.0f, 2.0f * c[1] - 1.0f, 2.0f * c[2] - 1.0f);
         dg.Ns = normalize(b.x * dg.Tx + b.y * dg.Ty + b.z * dg.Ns);
       }
       float d = m.p[0];
       if (m.tex[0] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], dg.s, dg.t, c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], dg.s, dg.t, c);
         d *= c[0];
       }
       if (d < 1.0f) add_comp(bs, C_TRANSMISSION, BT_SPECULAR_TRANSMISSION, v3s(1.0f - d));
       V3 Kd = d * v3(m.p[1], m.p[2], m.p[3]);
       if (m.tex[1] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[1], dg.s, dg.t, c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[1], dg.s, dg.t, c);
         Kd = Kd * v3(c[0], c[1], c[2]);
       }
       if (Kd != v3s(0.f)) add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, Kd);
       float Ns = m.p[7];
       if (m.tex[3] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[3], dg.s, dg.t, c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[3], dg.s, dg.t, c);
         Ns *= c[0];
       }
       V3 Ks = d * v3(m.p[4], m.p[5], m.p[6]);
       if (m.tex[2] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[2], dg.s, dg.t, c);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[2], dg.s, dg.t, c);
         Ks = Ks * v3(c[0], c[1], c[2]);
       }
       if (Ks != v3s(0.f)) add_comp(bs, C_SPECULAR, BT_GLOSSY_REFLECTION, Ks, Ns);
@@ -824,7 +824,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
       float alpha = 1.f, opacity = 0.f;
       if (m.tex[0] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
         alpha = dc[3];
         opacity = 1.f - alpha;
       }
@@ -841,7 +841,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[10], 1.0f);
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
       if (m.tex[0] >= 0)
-        tex_get(sv.textures, sv.images, sv.texels, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
       const float tr = m.p[9];
       const V3 T = v3(dc[0] * tr, dc[1] * tr, dc[2] * tr);
       add_comp(bs, C_THIN_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3(yrt_logf(T.x), yrt_logf(T.y), yrt_logf(T.z)), m.p[10],

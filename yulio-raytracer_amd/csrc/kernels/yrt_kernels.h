@@ -23,6 +23,7 @@ struct SceneView {
   const GpuTexture* textures;
   const GpuImage* images;
   const uint8_t* texels;
+  const uint8_t* texQuads;  // per 8-bit texel i: texels i, i+1, i+W, i+W+1 (16 B at 4x its texel offset)
   const GpuLight* lights;
   const int* envLights;
   const float* hdriDist;
