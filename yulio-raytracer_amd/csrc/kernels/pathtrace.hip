@@ -625,11 +625,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 // BackendSceneFlat::postIntersect -> Shape::postIntersect
 __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
                                bool wantTangents) {
-#if YRT_SHADE_FLAT
   const int g = sv.indices[gid].w;  // geometry id rides in the index record
-#else
-  const int g = sv.triGeom[gid];
-#endif
   const GpuGeom geom = sv.geoms[g];
   dg.material = geom.material;
   dg.light = geom.light;
@@ -1086,11 +1082,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     bool backfacing = false;
     if (active && isHit) {
       const int gid = __float_as_int(h.w);
-#if YRT_SHADE_FLAT
-      const int g = sv.indices[gid].w;
-#else
-      const int g = sv.triGeom[gid];
-#endif
+      const int g = sv.indices[gid].w;  // geometry id rides in the index record
       const int mat = sv.geoms[g].material;
       // tangents only feed the Obj bump map and the anisotropic microfacet
       const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && sv.materials[mat].type == MAT_OBJ &&

@@ -185,11 +185,6 @@ __device__ __forceinline__ void texel(const GpuImage& im, const uint8_t* __restr
   c[3] = im.format == IMG_RGB8 ? 1.0f : b.w * one_over_255;
 }
 
-// YRT_SHADE_FLAT: the texture record's own image descriptor and the triangle's geometry id
-// from its index record (indices[gid].w) — one dependent load fewer on each shading chain.
-#ifndef YRT_SHADE_FLAT
-#define YRT_SHADE_FLAT 1
-#endif
 // Texture::get (textures/Bilinear.h:8-25, textures/nearestneighbor.h:25-32) -> RGBA
 __device__ __forceinline__ void texel_u8(uint32_t w, bool rgb, float c[4]) {
   const float one_over_255 = 1.0f / 255.0f;
@@ -202,15 +197,13 @@ __device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures,
                                         const uint8_t* __restrict__ pool, const uint8_t* __restrict__ quads, int texId,
                                         float px, float py, float out[4]) {
   const GpuTexture tx = textures[texId];
-#if YRT_SHADE_FLAT
+  // the texture record carries its image's descriptor: one dependent load fewer (-2 % shade)
   GpuImage im;
   im.width = tx.width;
   im.height = tx.height;
   im.format = tx.format;
   im.offset = tx.offset;
-#else
-  const GpuImage im = images[tx.image];
-#endif
+  (void)images;
   const float s1 = px - floorf(px), t1 = py - floorf(py);
   float c[4];
   if (tx.filter == TEX_BILINEAR) {
@@ -296,11 +289,8 @@ __device__ __forceinline__ float aniso_D(float nx, float ny, const DG& dg, V3 wh
 
 // Microfacet<Fresnel, Distribution>::eval (brdfs/microfacet.h:28-41) for the dielectric /
 // conductor Fresnel terms and the power-cosine / anisotropic power-cosine distributions.
-// YRT_MICRO_SPEC: CM (the kernel's component set) compiles out the conductor / anisotropic
-// branches no material of the scene can create.
-#ifndef YRT_MICRO_SPEC
-#define YRT_MICRO_SPEC 1  // k_shade -5% on C3 (same-box A/B, profiles/r01)
-#endif
+// CM (the kernel's component set) compiles out the conductor / anisotropic branches no
+// material of the scene can create (k_shade -5 % on C3, same-box A/B, profiles/r01).
 template <unsigned CM>
 __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* __restrict__ mats, V3 wo, const DG& dg,
                                              V3 wi) {
@@ -311,8 +301,8 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* 
   const V3 wh = normalize(wi + wo);
   const float cosThetaH = dot(wh, dg.Ns);
   const float cosTheta = dot(wi, wh);
-  constexpr bool kCond = !YRT_MICRO_SPEC || (CM & (comp_bit(C_MICRO_COND) | comp_bit(C_MICRO_ANISO))) != 0;
-  constexpr bool kAniso = !YRT_MICRO_SPEC || (CM & comp_bit(C_MICRO_ANISO)) != 0;
+  constexpr bool kCond = (CM & (comp_bit(C_MICRO_COND) | comp_bit(C_MICRO_ANISO))) != 0;
+  constexpr bool kAniso = (CM & comp_bit(C_MICRO_ANISO)) != 0;
   const bool diel = !kCond || c.kind == C_MICROFACET;
   V3 F;
   if (diel) F = v3s(fresnel2(cosTheta, c.a * rcpf_(c.b), nullptr));

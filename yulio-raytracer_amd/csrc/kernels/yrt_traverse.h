@@ -40,10 +40,6 @@ static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK
 #define YRT_TRACE_BLOCK 64
 #endif
 
-#ifndef YRT_ASM_MINMAX
-#define YRT_ASM_MINMAX 1  // +1.5 % on C3 (shadow trace 5.84 -> 5.38 ms/launch), profiles/r02/trace_variants_r02.txt
-#endif
-
 namespace yrt {
 
 struct Hit {
@@ -149,9 +145,9 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
   const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz, oz2), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz, oz2);
 #undef YRT_SLAB
   const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
-#if YRT_ASM_MINMAX
-  // v_max/v_min written out: fmaxf/fminf on the loop-carried tnear / tfar make the compiler
-  // re-quiet (canonicalize) them with an extra v_max every node step (IEEE mode). A signalling
+  // v_max/v_min written out (+1.5 % on C3, shadow trace 5.84 -> 5.38 ms/launch,
+  // profiles/r02/trace_variants_r02.txt): fmaxf/fminf on the loop-carried tnear / tfar make
+  // the compiler re-quiet (canonicalize) them with an extra v_max every node step (IEEE mode). A signalling
   // NaN never reaches here (ray records are computed values), and the hardware min/max give
   // the same result as fmaxf/fminf for every other input.
 #define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                            \
@@ -164,15 +160,6 @@ __device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, floa
     t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;                  \
     c[k] = (CH);                                                                            \
   } while (0)
-#else
-#define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                    \
-  do {                                                                              \
-    const float nn = fmaxf(fmaxf(NX, NY), fmaxf(NZ, r.tnear));                      \
-    const float ff = fminf(fminf(FX, FY), fminf(FZ, tmax));                         \
-    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;          \
-    c[k] = (CH);                                                                    \
-  } while (0)
-#endif
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
   YRT_CHILD(1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y, ch.y);
   YRT_CHILD(2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x, ch.z);
