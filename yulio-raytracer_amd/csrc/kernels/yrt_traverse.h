@@ -210,6 +210,32 @@ __device__ __forceinline__ void sort3_far(float t[4], int c[4]) {
 #undef YRT_CSWAP_D
 }
 
+// One triangle without the distance range: true when the ray's line crosses the triangle
+// (barycentric and back-face tests); t, U, V, absDen as tri_test_t.
+__device__ __forceinline__ bool tri_test_g(const GpuTri& tr, const RayPre& r, float& t, float& U_, float& V_,
+                                           float& absDen_) {
+  V3 v0 = v3(tr.v0[0], tr.v0[1], tr.v0[2]);
+  V3 e1 = v3(tr.e1[0], tr.e1[1], tr.e1[2]);
+  V3 e2 = v3(tr.e2[0], tr.e2[1], tr.e2[2]);
+  V3 Ng = cross(e1, e2);
+  V3 C = v0 - r.org;
+  V3 R = cross(r.dir, C);
+  float den = dot(Ng, r.dir);
+  float absDen = fabsf(den);
+  float sgn = den < 0.0f ? -1.0f : 1.0f;
+  float U = dot(R, e2) * sgn;
+  float V = dot(R, e1) * sgn;
+  bool ok = (den != 0.0f) & (U >= 0.0f) & (V >= 0.0f) & (U + V <= absDen);
+  int flags = __float_as_int(tr.e1[3]);
+  ok &= !((flags & 1) && !(den > 0.0f));
+  float T = dot(Ng, C) * sgn;
+  t = T / absDen;
+  U_ = U;
+  V_ = V;
+  absDen_ = absDen;
+  return ok;
+}
+
 // One triangle; returns true and t when the ray hits within (tnear, tfar). U, V, absDen are
 // returned undivided: u = U/absDen, v = V/absDen are only needed for an accepted hit.
 __device__ __forceinline__ bool tri_test_t(const GpuTri& tr, const RayPre& r, float tfar, float& t, float& U_,
