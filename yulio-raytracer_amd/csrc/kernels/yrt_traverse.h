@@ -116,18 +116,38 @@ __device__ __forceinline__ int plane_offsets(float ix, float iy, float iz) {
 // of 82/84). nodeIdx < 2^25 (node byte offsets fit 32 bits; bvh_build.cpp enforces it).
 // MISS: the entry distance reported for a missed child (+INF for closest-hit rays, which sort
 // ascending; -INF for any-hit rays, which visit the farthest child first, see sort3_far).
-template <bool ANY = false>
-__device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
-                                             const GpuNode* __restrict__ base, int nodeIdx) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
+// The ray's near/far planes and the child references of one node, as loaded.
+struct NodeData {
+  float4 nx, fx, ny, fy, nz, fz;
+  int4 ch;
+};
+__device__ __forceinline__ NodeData node_load(const GpuNode* __restrict__ base, int nodeIdx, int planeOff) {
   const char* b0 = (const char*)base;
   const unsigned nb = (unsigned)nodeIdx << 7;
   const unsigned ox = (unsigned)planeOff & 0xffu, oy = ((unsigned)planeOff >> 8) & 0xffu,
                  oz = (unsigned)planeOff >> 16;
-  const float4 nx = *(const float4*)(b0 + (nb + ox)), fx = *(const float4*)(b0 + (nb + (16u - ox)));
-  const float4 ny = *(const float4*)(b0 + (nb + (32u + oy))), fy = *(const float4*)(b0 + (nb + (48u - oy)));
-  const float4 nz = *(const float4*)(b0 + (nb + (64u + oz))), fz = *(const float4*)(b0 + (nb + (80u - oz)));
-  const int4 ch = *(const int4*)(b0 + (nb + 96u));
+  NodeData d;
+  d.nx = *(const float4*)(b0 + (nb + ox));
+  d.fx = *(const float4*)(b0 + (nb + (16u - ox)));
+  d.ny = *(const float4*)(b0 + (nb + (32u + oy)));
+  d.fy = *(const float4*)(b0 + (nb + (48u - oy)));
+  d.nz = *(const float4*)(b0 + (nb + (64u + oz)));
+  d.fz = *(const float4*)(b0 + (nb + (80u - oz)));
+  d.ch = *(const int4*)(b0 + (nb + 96u));
+  return d;
+}
+template <bool ANY = false>
+__device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, float tmax, float t[4], int c[4]);
+template <bool ANY = false>
+__device__ __forceinline__ void box4_ordered(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
+                                             const GpuNode* __restrict__ base, int nodeIdx) {
+  box4_data<ANY>(node_load(base, nodeIdx, planeOff), r, tmax, t, c);
+}
+template <bool ANY>
+__device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, float tmax, float t[4], int c[4]) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const float4 nx = d.nx, fx = d.fx, ny = d.ny, fy = d.fy, nz = d.nz, fz = d.fz;
+  const int4 ch = d.ch;
   // slab distance t = fma(plane, inv, -org*inv): one fused op per plane instead of a subtract
   // and a multiply. Against (plane - org) * inv it carries an extra absolute error of at most
   // one rounding of org*inv (u * |oi|, u = 2^-24) on each of the near and far distances; the
