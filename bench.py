@@ -49,10 +49,14 @@ def parse():
     p.add_argument("--capture", type=int, default=4096,
                    help="rays per depth sampled for visit counts (0: no capture frame, e.g. PMC passes)")
     p.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
-    p.add_argument("--stereo-frames", type=int, default=0,
-                   help="C4 stereo cubemaps (12 x 1536^2 x 256spp, tile split over the ranks) timed after the "
-                        "main loop and reported under 'stereo_cubemap'. Off by default so a rocprof summary "
-                        "of the default command averages only the C3 launches of the roofline kernel")
+    p.add_argument("--stereo-size", type=int, default=1536, help="cube face size (C4: 1536; smaller for tests)")
+    p.add_argument("--stereo-spp", type=int, default=256, help="cube spp (C4: 256; smaller for tests)")
+    p.add_argument("--stereo-frames", type=int, default=None,
+                   help="C4 stereo cubemaps (12 x 1536^2 x 256spp, one job, tiles dealt over the ranks) timed "
+                        "after the main loop and reported under 'stereo_cubemap'. Default: 1 at N>1 (the "
+                        "BASELINE 1/2/4/8-GPU cubemap, gather checked against a one-GPU render), 0 at N=1 so "
+                        "a rocprof summary of the default command averages only the C3 launches of the "
+                        "roofline kernel")
     return p.parse_args()
 
 
@@ -69,11 +73,14 @@ def main():
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
+    if a.stereo_frames is None:
+        a.stereo_frames = 1 if world > 1 else 0
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    gpus_used = physical_gpus(world, local)
 
     import yrt
     from yrt import standin
@@ -155,7 +162,7 @@ def main():
     rays, closest, shadow = tot.tolist()
     elapsed = tmax.item()
 
-    stereo = stereo_cubemap(a, dev, rank, world, backend, gather) if a.stereo_frames > 0 else None
+    stereo = stereo_cubemap(a, dev, rank, world, backend, gather, local) if a.stereo_frames > 0 else None
 
     if rank == 0:
         # dominant trace kernel: what binds it. The BVH and the
@@ -203,7 +210,8 @@ def main():
             "metric": f"Mrays/s (Sponza stand-in {a.size}^2 {a.spp}spp, closest+shadow queries)",
             "value": round(rays / elapsed / 1e6, 2),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": gpus_used,
+            "ranks": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 2),
@@ -225,6 +233,20 @@ def main():
     dev.close()
     if world > 1:
         dist.destroy_process_group()
+    if stereo and stereo.get("gather_check") not in (None, "bit_exact"):
+        sys.exit(f"stereo cubemap gather check failed: {stereo['gather_check']}")
+
+
+def physical_gpus(world, local):
+    """Distinct GPUs the ranks run on (host, HIP device): the gloo rehearsal puts several
+    ranks on one GPU, the driver's N-GPU runs one rank per GPU."""
+    if world == 1:
+        return 1
+    import socket
+    import torch.distributed as dist
+    keys = [None] * world
+    dist.all_gather_object(keys, (socket.gethostname(), local))
+    return len(set(keys))
 
 
 def setup_gather(dev, rank, world, backend):
@@ -240,8 +262,13 @@ def setup_gather(dev, rank, world, backend):
     err = "" if backend == "nccl" else f"backend {backend}"
     uid = None
     if not err:
-        try:  # every rank first checks that librccl loads (a rank failing inside the
-            uid = dev.shard_comm_unique_id()  # collective ncclCommInitRank would hang the others)
+        # every rank first checks that librccl loads (a rank failing inside the collective
+        # ncclCommInitRank would hang the others); only rank 0 makes the unique id
+        try:
+            if rank == 0:
+                uid = dev.shard_comm_unique_id()
+            elif not dev.rccl_available():
+                err = "librccl cannot be loaded"
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             err = str(e)[:200]
     ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dd)
@@ -335,36 +362,48 @@ def cpu_info():
             "cgroup_cpu_quota": quota}
 
 
-def stereo_cubemap(a, dev, rank, world, backend, gather):
+def stereo_cubemap(a, dev, rank, world, backend, gather, local):
     """BASELINE.json configs[3]: the test_stereo stereo cubemap (12 faces x 1536^2, 256 spp,
-    depth 10, test_stereo_view.ecs), every face's 16x16 tiles dealt round-robin over the
-    ranks, the faceCamera billboard refit per face, and one RCCL reduce of the
-    12 RGB8 faces (disjoint tiles) to rank 0 at the end. Strong scaling: the cubemap is the
-    same at every N; Mrays/s = closest + shadow queries of all ranks / max-over-ranks time."""
+    depth 10, test_stereo_view.ecs) as one job per cubemap (yrtRenderFrames): the 110,592
+    16x16 tiles of the 12 faces dealt round-robin over the ranks and gathered on
+    rank 0 by the device's RCCL send/recv inside the call. Strong scaling: the same cubemap at
+    every N; Mrays/s = closest + shadow queries of all ranks / max-over-ranks time.
+
+    Untimed check at N>1: rank 0 renders the same cubemap alone (a second device on its GPU, no
+    sharding) and compares it with the gathered one byte for byte (gather_check); that render's
+    time is the same-box one-GPU reference of the strong-scaling line."""
     import torch
     import torch.distributed as dist
     import yrt
-    scenes = ROOT / "scenes"
-    ses = yrt.Session(["-i", str(scenes / "test_stereo.xml"), "-c", str(scenes / "test_stereo_view.ecs"),
-                       "-size", "1536", "1536", "-spp", "256", "-stereo"], device=dev)
+    args = ["-i", str(ROOT / "scenes" / "test_stereo.xml"), "-c", str(ROOT / "scenes" / "test_stereo_view.ecs"),
+            "-size", str(a.stereo_size), str(a.stereo_size), "-spp", str(a.stereo_spp), "-stereo"]
+    ses = yrt.Session(args, device=dev)
     info = ses.info()
     W, H = info["width"], info["height"]
     stride = (3 * W + 3) // 4 * 4
-    faces = torch.zeros((12, stride * H), dtype=torch.uint8, device="cuda" if backend == "nccl" else "cpu")
-    ses.render(0)  # untimed: allocations, sample table
+    cxx = gather.startswith("C++") or world == 1
+    faces_t = None
+    if not cxx:
+        faces_t = torch.zeros((12, stride * H), dtype=torch.uint8, device="cuda" if backend == "nccl" else "cpu")
+
+    def one_cube():
+        if cxx:
+            ses.render_cube(read=False)
+        else:  # fallback: every rank's faces (zero outside its tiles) summed on rank 0
+            for f, img in enumerate(ses.render_cube()):
+                faces_t[f].copy_(torch.from_numpy(rgb8_rows(img, stride)))
+            dist.reduce(faces_t, dst=0, op=dist.ReduceOp.SUM)
+        st = dev.render_stats()
+        return st["raysClosest"] + st["raysShadow"]
+
+    one_cube()  # untimed: allocations, sample table
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     rays = 0.0
     t0 = time.perf_counter()
     for _ in range(a.stereo_frames):
-        for f in range(12):
-            img = ses.render(f)
-            st = dev.render_stats()
-            rays += st["raysClosest"] + st["raysShadow"]
-            faces[f, :img.size].copy_(torch.from_numpy(np.ascontiguousarray(img).reshape(-1)))
-        if world > 1 and not gather.startswith("C++"):
-            dist.reduce(faces, dst=0, op=dist.ReduceOp.SUM)
+        rays += one_cube()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -375,14 +414,56 @@ def stereo_cubemap(a, dev, rank, world, backend, gather):
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-    ses.close()
     dt = tm.item()
-    samples = 12.0 * W * H * 256 * a.stereo_frames
-    return {"metric": "Mrays/s (test_stereo stereo cubemap 12x1536^2 256spp, closest+shadow queries)",
-            "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": world,
-            "scaling": "strong", "ms_per_cubemap": round(dt / a.stereo_frames * 1e3, 1),
-            "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
-            "parallelism": f"face-tiles-roundrobin{world}"}
+    samples = 12.0 * W * H * a.stereo_spp * a.stereo_frames
+    c4 = (W, a.stereo_spp) == (1536, 256)
+    out = {"metric": f"Mrays/s (test_stereo stereo cubemap 12x{W}^2 {a.stereo_spp}spp, closest+shadow queries)",
+           "workload": "C4" if c4 else "C4-reduced",
+           "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": world,
+           "scaling": "strong", "ms_per_cubemap": round(dt / a.stereo_frames * 1e3, 1),
+           "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
+           "parallelism": f"cube-tiles-roundrobin{world}", "gather": "C++ RCCL" if cxx else "torch reduce",
+           "gather_check": None}
+    if world > 1:
+        # the gathered cubemap (rank 0) against a one-GPU render of the same cubemap
+        got = None
+        if rank == 0:
+            got = [rgb8_rows(img, stride) for img in ses._cube_faces()] if cxx else \
+                [faces_t[f].cpu().numpy() for f in range(12)]
+        check = single_gpu_cube(args, local, stride) if rank == 0 else None
+        if rank == 0:
+            ref, t_single = check
+            bad = sum(int(np.count_nonzero(g != r)) for g, r in zip(got, ref))
+            out["gather_check"] = "bit_exact" if bad == 0 else f"{bad} bytes differ"
+            out["single_gpu_ms_per_cubemap"] = round(t_single * 1e3, 1)
+            out["strong_scaling_efficiency"] = round(t_single / (world * dt / a.stereo_frames), 3)
+        dist.barrier()
+    ses.close()
+    return out
+
+
+def rgb8_rows(img, stride):
+    """An (H, W, 3) RGB8 face as the framebuffer's padded rows (api/framebuffer.h:194-226)."""
+    h, w, _ = img.shape
+    rows = np.zeros((h, stride), np.uint8)
+    rows[:, :3 * w] = img.reshape(h, 3 * w)
+    return rows.reshape(-1)
+
+
+def single_gpu_cube(args, local, stride):
+    """Rank 0's reference: the cubemap rendered by an unsharded device on its own GPU (timed,
+    after one warm-up render)."""
+    import yrt
+    d1 = yrt.Device(local)
+    s1 = yrt.Session(args, device=d1)
+    s1.render_cube(read=False)
+    t = time.perf_counter()
+    s1.render_cube(read=False)
+    dt = time.perf_counter() - t
+    ref = [rgb8_rows(img, stride) for img in s1._cube_faces()]
+    s1.close()
+    d1.close()
+    return ref, dt
 
 
 def cpu_baseline(ses, a):

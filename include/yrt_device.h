@@ -110,6 +110,16 @@ YRT_API int yrtCommit(YRTDevice dev, YRTHandle h);
 /* ---- rendering (device.h:223-234, 322) ----------------------------------------------- */
 YRT_API int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene,
                            YRTHandle tonemapper, YRTHandle framebuffer, int accumulate);
+/* Several frames of one scene in one wavefront job: frame k seen through cameras[k] into
+ * framebuffers[k] (all the same size and format). The result equals numFrames rtRenderFrame
+ * calls with the same accumulate flag, bit for bit (the per-tile Random of
+ * integratorrenderer.cpp:134 and every per-pixel input depend on the frame's own pixel only),
+ * but the frames' 16x16 tiles form one sequence (frame-major) that fills the batches and is
+ * dealt over shards and GPUs as a whole, with one gather per job. This is the loop of the
+ * stereo-cube drivers over the 12 faces of a view (renderer.cpp:543-737, 742-878) when no
+ * primitive changes between the faces. */
+YRT_API int yrtRenderFrames(YRTDevice dev, YRTHandle renderer, const YRTHandle* cameras, int numFrames,
+                            YRTHandle scene, YRTHandle tonemapper, const YRTHandle* framebuffers, int accumulate);
 YRT_API void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
 YRT_API int yrtUnmapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
 YRT_API int yrtSwapBuffers(YRTDevice dev, YRTHandle framebuffer);
@@ -175,7 +185,8 @@ YRT_API int yrtSetFrameSeed(YRTDevice dev, uint32_t seed);
 YRT_API int yrtSetBatchCapacity(YRTDevice dev, int64_t paths);
 /* Tile sharding across processes: this process renders only the tiles with
  * (tileIndex % count) == index (dealt further over its own HIP devices, see yrtNewDevice);
- * without a communicator (yrtSetShardComm) the other tiles' pixels are left zero. */
+ * without a communicator (yrtSetShardComm) the other tiles' pixels are left zero. With a
+ * communicator, only its own (rank, world) shard is accepted. */
 YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
 /* Multi-GPU, one process per GPU (the reference's device_network image split,
  * devices/device_network/network_device.cpp:255-300, as an RCCL gather over xGMI):
@@ -184,7 +195,15 @@ YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
  * (tile % world == rank) and every rtRenderFrame ends with a grouped RCCL send of each rank's
  * tile slab to rank 0, whose framebuffer then holds the whole frame. */
 YRT_API int yrtShardCommUniqueId(void* id128);
+/* Every rank of a job calls yrtSetShardComm (collective: RCCL ncclCommInitRank). Before each
+ * gather the ranks exchange their render status, so a rank whose render throws makes every
+ * rank's yrtRenderFrame fail instead of leaving rank 0 waiting. world = 1 drops the
+ * communicator. The gathered slabs carry 4 bytes per pixel for RGB8 framebuffers (16 else).
+ * Only rank 0's framebuffers receive pixels; the other ranks' host framebuffers are left as
+ * they were (their part of the frame is already on rank 0). */
 YRT_API int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128);
+/* 1 when librccl can be loaded (checked on every rank before the collective comm init). */
+YRT_API int yrtRcclAvailable(void);
 /* HIP devices (logical shards) this device renders on (yrtNewDevice "devices=..."). */
 YRT_API int yrtGetDeviceCount(YRTDevice dev);
 /* Scene commits that only move the vertices of some primitives (faceCamera re-orientation by

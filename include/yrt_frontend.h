@@ -48,6 +48,14 @@ YRT_API void* yrtSessionRenderSceneCamera(YRTSession s, int i);
 /* Renders one frame (mono: face -1) into the session framebuffer and returns the mapped
  * host pointer (format per yrtSessionInfo). */
 YRT_API void* yrtSessionRender(YRTSession s, int face);
+/* The 12 stereo cube faces (renderer.cpp:742-878) rendered as one job (yrtRenderFrames) into
+ * 12 session-owned framebuffers (yrtSessionCubeFrameBuffer(s, face)). Returns 0 / -1. */
+YRT_API int yrtSessionRenderCube(YRTSession s);
+/* The 12 faces of FPR view `view` (scene cameras 12*view .. 12*view+11) as one job: the
+ * faceCamera primitives re-oriented once toward the view's camera origin, the scene
+ * re-committed, then yrtRenderFrames (renderer.cpp:543-576 for the whole view). */
+YRT_API int yrtSessionRenderSceneCube(YRTSession s, int view);
+YRT_API YRTHandle yrtSessionCubeFrameBuffer(YRTSession s, int face);
 /* outputMode(-o file): renders and stores the image (.ppm/.pfm/.png; stereo: 12-face strip;
  * with Collada cameras the FPR branch: <dir>/<name>_<camera>.jpg per view, file ignored). */
 YRT_API int yrtSessionOutput(YRTSession s, const char* file);

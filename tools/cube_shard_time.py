@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""GPU-box: strong-scaling prediction of the stereo cubemaps on ONE GPU.
+
+For N = 1, 2, 4, 8 the cubemap's 16x16 tiles are dealt round-robin over N ranks (SURVEY
+§8(e)); this times rank r's share (yrtSetTileShard(r, N)) of one full cubemap, the way that
+rank renders it in an N-GPU run, minus the RCCL gather. The predicted N-GPU time of a cubemap
+is the slowest share; efficiency = T(1) / (N * T(N)).
+
+  C4: test_stereo.ecs stereo cubemap, 12 x 1536^2 at 256 spp (non-FPR stereo branch,
+      renderer.cpp:742-878)
+  C5: the Frederick stand-in (yrt.frederick) FPR view, 12 x 1536^2 at 1024 spp (renderer.cpp:
+      543-737: faceCamera update, scene commit, render)
+
+--mode face: one rtRenderFrame per face (the reference's loop);
+--mode cube: the 12 faces in one yrtRenderFrames call (tiles of all faces in one sequence).
+
+usage: python tools/cube_shard_time.py C4|C5 [--mode face|cube] [--gpus 1,2,4,8] [--ranks all|0]
+       [--spp N] [--size S]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "yulio-raytracer_amd"), str(ROOT), str(ROOT / "tests")]
+
+import yrt  # noqa: E402
+
+
+def session(cfg, dev, size, spp):
+    if cfg == "C4":
+        from helpers import c4_args
+        return yrt.Session(c4_args(size, spp), device=dev)
+    from yrt import frederick
+    dae = frederick.write_dae(ROOT / "scenes" / "_generated" / "frederick_c5" / "frederick.dae")
+    return yrt.Session(["-fprCollada", "-faceCullingMode", "default", "-i", str(dae), "-stereo", "-size", str(size),
+                        str(size), "-spp", str(spp), "-depth", "10", "-tMaxShadowRay", "120", "-ambientlight",
+                        "0.83", "0.95", "0.98", "-toeIn"], device=dev)
+
+
+def render_cube(ses, cfg, mode):
+    """One full cubemap; returns rays traced (closest + shadow)."""
+    dev = ses.device
+    if mode == "cube":
+        if cfg == "C4":
+            ses.render_cube()
+        else:
+            ses.render_scene_cube(0)
+        st = dev.render_stats()
+        return st["raysClosest"] + st["raysShadow"]
+    rays = 0.0
+    for f in range(12):
+        if cfg == "C4":
+            ses.render(f)
+        else:
+            ses.render_scene_camera(f)
+        st = dev.render_stats()
+        rays += st["raysClosest"] + st["raysShadow"]
+    return rays
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cfg", choices=["C4", "C5"])
+    ap.add_argument("--mode", choices=["face", "cube"], default="face")
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to time")
+    ap.add_argument("--size", type=int, default=1536)
+    ap.add_argument("--spp", type=int, default=0, help="0: the config's own (C4 256, C5 1024)")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    spp = a.spp or (256 if a.cfg == "C4" else 1024)
+    dev = yrt.Device(0)
+    ses = session(a.cfg, dev, a.size, spp)
+    render_cube(ses, a.cfg, a.mode)  # untimed: allocations, sample table, BVH
+    rows = []
+    t1 = None
+    for n in [int(x) for x in a.gpus.split(",")]:
+        ranks = range(n) if a.ranks == "all" else [int(r) for r in a.ranks.split(",") if int(r) < n]
+        times = {}
+        rays = 0.0
+        for r in ranks:
+            dev.set_tile_shard(r, n)
+            t = time.perf_counter()
+            rays += render_cube(ses, a.cfg, a.mode)
+            times[r] = time.perf_counter() - t
+            print(f"{a.cfg} {a.mode} N={n} rank {r}: {times[r] * 1e3:.1f} ms", flush=True)
+        tmax = max(times.values())
+        if n == 1:
+            t1 = tmax
+        row = {"config": a.cfg, "mode": a.mode, "n": n, "ranks_timed": list(times), "ms_max": round(tmax * 1e3, 1),
+               "ms_mean": round(sum(times.values()) / len(times) * 1e3, 1),
+               "ms_per_rank": {str(k): round(v * 1e3, 1) for k, v in times.items()},
+               "predicted_efficiency": round(t1 / (n * tmax), 3) if t1 else None,
+               "Mrays_per_s_per_gpu": round(rays / sum(times.values()) / 1e6, 1)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    dev.set_tile_shard(0, 1)
+    ses.close()
+    dev.close()
+    if a.out:
+        Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.out).write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+
+
+if __name__ == "__main__":
+    main()

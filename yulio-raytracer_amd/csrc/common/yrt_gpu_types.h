@@ -117,7 +117,10 @@ struct GpuRenderParams {
   int32_t dim2D, lightSampleID, firstScatterSampleID, firstScatterTypeSampleID;
   int32_t width, height, numTilesX, numTilesY;
   float rcpWidth, rcpHeight, gamma, rcpGamma;
-  uint32_t frameSeed, pad[3];
+  uint32_t frameSeed;
+  // frames rendered together (yrtRenderFrames: the 12 faces of a stereo cubemap): tile t of
+  // the job is tile t % tilesPerFrame of frame t / tilesPerFrame (numTilesX * numTilesY each)
+  int32_t numFrames, tilesPerFrame, pad;
 };
 
 // Camera (cameras/pinholecamera.h:15-21, cameras/StereoCubeCamera.h:16-65).

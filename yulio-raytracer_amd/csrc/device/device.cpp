@@ -61,8 +61,9 @@ struct GpuCtx {
   Lane lanes[kMaxLanes];
   int numLanes = kMaxLanes;
   DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab;
+  std::vector<GpuCamera> hCams;  // the job's cameras, one per frame (uploaded to dCam)
   DevBuf dBackplate;                       // the renderer's backplate image (texels)
-  const ImageObj* backplateKey = nullptr;  // the image dBackplate holds
+  uint64_t backplateSerial = 0;            // ImageObj::serial of the image dBackplate holds
   std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
@@ -170,6 +171,8 @@ class Device {
   // t = shardIndex (mod shardCount), dealt over its own devices
   int shardIndex = 0, shardCount = 1;
   ncclComm_t procComm = nullptr;     // process-level gather to rank 0 (yrtSetShardComm)
+  int commRank = 0, commWorld = 1;   // procComm's rank / size: the only shard it gathers
+  DevBuf dCommFlag;                  // per-frame render status exchanged before the gather
   ncclComm_t localComm = nullptr;    // the ctx devices' gather (distinct devices only): rank 0's
   std::vector<ncclComm_t> localComms;  // one per ctx device (ncclCommInitAll)
   bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
@@ -231,11 +234,14 @@ class Device {
     return *r;
   }
 
-  void render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F, int accumulate);
-  void render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, ToneMapperObj& T, int W, int H,
-                    int index, int count, int accumulate, bool reportProgress);
-  void gather_local(int W, int H, int numTiles);
-  void gather_process(int W, int H, int numTiles);
+  // one or several frames of the same size and format in one wavefront job (yrtRenderFrames):
+  // their tiles form one sequence, frame-major, dealt over shards and devices
+  void render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& S, ToneMapperObj& T,
+              const std::vector<FrameBufferObj*>& F, int accumulate);
+  void render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vector<CameraObj*>& C, ToneMapperObj& T,
+                    int W, int H, int index, int count, int accumulate, bool reportProgress);
+  void gather_local(const SlabLayout& base, int numTiles);
+  void gather_process(const SlabLayout& base, int numTiles, bool localOk);
   void intersect(SceneObj& S, const float* org4, const float* dir4, uint32_t n, float* hit4, int32_t* occ,
                  hipStream_t st);
 };
@@ -245,40 +251,72 @@ static void status(RendererObj& R, int state, float progress) {
   if (R.statusCallback) ((YRTStatusCallback)R.statusCallback)(state, progress, R.statusUser);
 }
 
-void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T, FrameBufferObj& F,
-                    int accumulate) {
+void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& S, ToneMapperObj& T,
+                    const std::vector<FrameBufferObj*>& F, int accumulate) {
   auto t0 = std::chrono::steady_clock::now();
-  if (!S.gpu) throw std::runtime_error("scene not committed");
-  if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
-  const int W = F.width, H = F.height;
-  const int numTiles = ((W + 15) / 16) * ((H + 15) / 16);
-  memset(&stats, 0, sizeof(stats));
-  if (!accumulate) R.iteration = 0;
+  // A process-level gather (yrtSetShardComm) is collective: every rank must reach it, so any
+  // failure of this rank's part (arguments, scene, kernels) is reported to the peers through
+  // the status exchange at its start instead of being thrown past it.
+  const bool procGather = !R.debug && procComm && shardCount > 1 && shardIndex == commRank && shardCount == commWorld;
+  const int nf = (int)F.size();
+  const int W = nf ? F[0]->width : 0, H = nf ? F[0]->height : 0;
+  const int tilesPerFrame = ((W + 15) / 16) * ((H + 15) / 16);
+  const int numTiles = tilesPerFrame * nf;
+  const bool rgb8 = nf && F[0]->format == FB_RGB8;
+  SlabLayout base{W, H, (3 * W + 3) / 4 * 4, tilesPerFrame, 0, 1, rgb8 ? 1 : 0, 0};
   const int N = (int)ctx.size();
   // the debug renderer is a one-pass traversal KAT: the primary device renders every tile
   const int nr = R.debug ? 1 : N;
-  std::vector<GpuScene*> scenes(nr);
-  for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
-  if (nr == 1) {
-    render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
-  } else {
-    // device k of this process renders the tiles t = shardIndex + k * shardCount (mod shardCount * N)
-    std::vector<std::string> errs(nr);
-    std::vector<std::thread> th;
-    for (int k = 0; k < nr; ++k)
-      th.emplace_back([&, k] {
-        try {
-          render_shard(*ctx[k], *scenes[k], R, C, T, W, H, shardIndex + k * shardCount, shardCount * nr, accumulate,
-                       k == 0);
-        } catch (const std::exception& e) {
-          errs[k] = e.what();
-        }
-      });
-    for (auto& t : th) t.join();
-    for (auto& e : errs)
-      if (!e.empty()) throw std::runtime_error(e);
-    gather_local(W, H, numTiles);
+  std::string localErr;
+  try {
+    if (!S.gpu) throw std::runtime_error("scene not committed");
+    if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
+    if (nf < 1 || (int)C.size() != nf) throw std::runtime_error("rtRenderFrames: one camera per framebuffer");
+    for (const FrameBufferObj* f : F)
+      if (f->width != W || f->height != H || f->format != F[0]->format)
+        throw std::runtime_error("rtRenderFrames: framebuffers differ in size or format");
+    if (R.debug && nf > 1) {
+      // the debug renderer is a one-frame traversal KAT: its frames go one by one
+      YRTRenderStats acc{};
+      for (int k = 0; k < nf; ++k) {
+        render(R, {C[k]}, S, T, {F[k]}, accumulate);
+        acc.raysClosest += stats.raysClosest;
+        acc.samples += stats.samples;
+      }
+      acc.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      stats = acc;
+      return;
+    }
+    memset(&stats, 0, sizeof(stats));
+    if (!accumulate) R.iteration = 0;
+    std::vector<GpuScene*> scenes(nr);
+    for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
+    if (nr == 1) {
+      render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
+    } else {
+      // device k of this process renders the tiles t = shardIndex + k * shardCount (mod shardCount * N)
+      std::vector<std::string> errs(nr);
+      std::vector<std::thread> th;
+      for (int k = 0; k < nr; ++k)
+        th.emplace_back([&, k] {
+          try {
+            render_shard(*ctx[k], *scenes[k], R, C, T, W, H, shardIndex + k * shardCount, shardCount * nr,
+                         accumulate, k == 0);
+          } catch (const std::exception& e) {
+            errs[k] = e.what();
+          }
+        });
+      for (auto& t : th) t.join();
+      for (auto& e : errs)
+        if (!e.empty()) throw std::runtime_error(e);
+      gather_local(base, numTiles);
+    }
+  } catch (const std::exception& e) {
+    if (!procGather) throw;
+    localErr = e.what();
   }
+  if (procGather) gather_process(base, numTiles, localErr.empty());
+  if (!localErr.empty()) throw std::runtime_error(localErr);
   R.iteration++;
   for (int k = 0; k < nr; ++k) {
     const YRTRenderStats& s = ctx[k]->stats;
@@ -290,21 +328,28 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     stats.msTraceShadow = std::max(stats.msTraceShadow, s.msTraceShadow);
     stats.msShade = std::max(stats.msShade, s.msShade);
   }
-  if (!R.debug && shardCount > 1 && procComm) gather_process(W, H, numTiles);
 
-  // framebuffer write-back (api/framebuffer.h:93-226) from the primary device
+  // framebuffer write-back (api/framebuffer.h:93-226) from the primary device, frame by frame.
+  // The other ranks of a process gather hold only their tiles: their host pixels are not
+  // written (rank 0's framebuffers receive the gathered frames).
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  void* dst = F.buffer(F.cur);
-  if (F.format == FB_RGB8) {
-    HIP_CHECK(hipMemcpy(dst, g0.dFbRGB8.p, rgb8Stride * H, hipMemcpyDeviceToHost));
-  } else {
-    std::vector<float> tmp((size_t)W * H * 3);
-    HIP_CHECK(hipMemcpy(tmp.data(), g0.dFbFloat.p, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
-    if (F.format == FB_RGB_FLOAT32) {
+  std::vector<float> tmp;
+  for (int k = 0; k < nf && !(procGather && shardIndex != 0); ++k) {
+    FrameBufferObj& Fk = *F[k];
+    void* dst = Fk.buffer(Fk.cur);
+    if (Fk.format == FB_RGB8) {
+      HIP_CHECK(hipMemcpy(dst, g0.dFbRGB8.as<uint8_t>() + (size_t)k * rgb8Stride * H, rgb8Stride * H,
+                          hipMemcpyDeviceToHost));
+      continue;
+    }
+    tmp.resize((size_t)W * H * 3);
+    HIP_CHECK(hipMemcpy(tmp.data(), g0.dFbFloat.as<float>() + (size_t)k * W * H * 3, tmp.size() * sizeof(float),
+                        hipMemcpyDeviceToHost));
+    if (Fk.format == FB_RGB_FLOAT32) {
       memcpy(dst, tmp.data(), tmp.size() * sizeof(float));
-    } else if (F.format == FB_RGBA_FLOAT32) {
+    } else if (Fk.format == FB_RGBA_FLOAT32) {
       float* o = (float*)dst;
       for (size_t i = 0; i < (size_t)W * H; ++i) {
         o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
@@ -312,7 +357,7 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
     } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
       uint8_t* o = (uint8_t*)dst;
       for (size_t i = 0; i < (size_t)W * H; ++i) {
-        for (int k = 0; k < 3; ++k) o[4 * i + k] = (uint8_t)clampf(tmp[3 * i + k] * 255.0f, 0.0f, 255.0f);
+        for (int c = 0; c < 3; ++c) o[4 * i + c] = (uint8_t)clampf(tmp[3 * i + c] * 255.0f, 0.0f, 255.0f);
         o[4 * i + 3] = 0;
       }
     }
@@ -324,8 +369,9 @@ void Device::render(RendererObj& R, CameraObj& C, SceneObj& S, ToneMapperObj& T,
 
 // Renders the tiles of shard (index, count) of the frame into g's full-size buffers (the other
 // tiles' pixels are left zero when count > 1).
-void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, ToneMapperObj& T, int W, int H,
-                          int index, int count, int accumulate, bool reportProgress) {
+void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vector<CameraObj*>& C,
+                          ToneMapperObj& T, int W, int H, int index, int count, int accumulate, bool reportProgress) {
+  const int nf = (int)C.size();
   HIP_CHECK(hipSetDevice(g.hipDevice));
   memset(&g.stats, 0, sizeof(g.stats));
   SceneView sv = G.view;
@@ -353,6 +399,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
   rp.numLights = G.view.numLights;
   rp.numEnvLights = G.view.numEnvLights;
   rp.numPrecomp = (int)G.precomputed.size();
+  rp.numFrames = nf;
+  rp.tilesPerFrame = rp.numTilesX * rp.numTilesY;
 
   // samples: PathTraceIntegrator::requestSamples (pathtraceintegrator.cpp:35-47)
   SampleRequest req;
@@ -391,16 +439,18 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
   rp.sets = tab.sets;
 
   g.dRp.alloc(sizeof(rp));
-  g.dCam.alloc(sizeof(GpuCamera));
+  g.hCams.resize(nf);
+  for (int k = 0; k < nf; ++k) g.hCams[k] = C[k]->cam;
+  g.dCam.alloc(sizeof(GpuCamera) * nf);
   HIP_CHECK(hipMemcpyAsync(g.dRp.p, &rp, sizeof(rp), hipMemcpyHostToDevice, stream));
-  HIP_CHECK(hipMemcpyAsync(g.dCam.p, &C.cam, sizeof(GpuCamera), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(g.dCam.p, g.hCams.data(), sizeof(GpuCamera) * nf, hipMemcpyHostToDevice, stream));
   g.dPixelSets.alloc((size_t)W * H);
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  g.dFbFloat.alloc((size_t)W * H * 3 * sizeof(float));
-  g.dFbRGB8.alloc(rgb8Stride * H);
+  g.dFbFloat.alloc((size_t)nf * W * H * 3 * sizeof(float));
+  g.dFbRGB8.alloc((size_t)nf * rgb8Stride * H);
   if (count > 1) {  // pixels of other shards stay 0 so per-shard images compose by sum
-    HIP_CHECK(hipMemsetAsync(g.dFbFloat.p, 0, (size_t)W * H * 3 * sizeof(float), stream));
-    HIP_CHECK(hipMemsetAsync(g.dFbRGB8.p, 0, rgb8Stride * H, stream));
+    HIP_CHECK(hipMemsetAsync(g.dFbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
+    HIP_CHECK(hipMemsetAsync(g.dFbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));
   }
 
   FrameView fv;
@@ -415,9 +465,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
   fv.backplateTexels = nullptr;
   if (R.backplate && !R.debug) {
     const ImageObj& im = *R.backplate;
-    if (g.backplateKey != &im || g.dBackplate.bytes < im.data.size()) {
+    if (g.backplateSerial != im.serial) {
       g.dBackplate.upload(im.data);
-      g.backplateKey = &im;
+      g.backplateSerial = im.serial;
     }
     fv.backplate.width = im.width;
     fv.backplate.height = im.height;
@@ -427,7 +477,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
   }
 
   if (reportProgress) status(R, 1, 0.f);
-  const int numTiles = rp.numTilesX * rp.numTilesY;
+  const int numTiles = rp.tilesPerFrame * nf;
   const int shardTiles = shard_tiles(numTiles, index, count);
 
   if (R.debug) {
@@ -452,7 +502,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
     const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
     const size_t counterWords = qcounter_index(levels, 0, 0);
-    g.dAccu.alloc((size_t)W * H * 16);
+    g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
       GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights);
@@ -587,29 +637,31 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, CameraObj& C, 
     g.eventPool.clear();
   }
   for (int l = 0; l < GpuCtx::kMaxLanes; ++l) HIP_CHECK(hipStreamSynchronize(g.lanes[l].stream));
-  g.stats.samples = (double)W * H * (R.debug ? 1 : rp.spp);
+  g.stats.samples = (double)nf * W * H * (R.debug ? 1 : rp.spp);
 }
 
 // The ctx devices' shards onto ctx[0]: every peer packs its tiles into a slab, the slabs go to
 // the first device (RCCL grouped send/recv when the devices are distinct GPUs — one xGMI link
 // per peer; a device-to-device copy when logical shards share a GPU) and are unpacked there.
-void Device::gather_local(int W, int H, int numTiles) {
+void Device::gather_local(const SlabLayout& base, int numTiles) {
   const int N = (int)ctx.size();
-  const int rgb8Stride = (3 * W + 3) / 4 * 4;
   bool distinct = true;
   for (int a = 0; a < N; ++a)
     for (int b = a + 1; b < N; ++b) distinct &= ctx[a]->hipDevice != ctx[b]->hipDevice;
   GpuCtx& g0 = *ctx[0];
+  const size_t eb = slab_element_bytes(base.rgb8);
   std::vector<int> tiles(N);
+  std::vector<SlabLayout> lay(N, base);
   for (int k = 1; k < N; ++k) {
     GpuCtx& g = *ctx[k];
-    tiles[k] = shard_tiles(numTiles, shardIndex + k * shardCount, shardCount * N);
+    lay[k].tileOffset = shardIndex + k * shardCount;
+    lay[k].tileStride = shardCount * N;
+    tiles[k] = shard_tiles(numTiles, lay[k].tileOffset, lay[k].tileStride);
     HIP_CHECK(hipSetDevice(g.hipDevice));
-    g.dSlab.alloc((size_t)std::max(1, tiles[k]) * 256 * sizeof(float4));
-    launch_pack_tiles(g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), W, H, rgb8Stride, shardIndex + k * shardCount,
-                      shardCount * N, tiles[k], g.dSlab.as<float4>(), g.stream);
+    g.dSlab.alloc((size_t)std::max(1, tiles[k]) * 256 * eb);
+    launch_pack_tiles(g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), lay[k], tiles[k], g.dSlab.p, g.stream);
     HIP_CHECK(hipSetDevice(g0.hipDevice));
-    g0.recvSlabs[k].alloc((size_t)std::max(1, tiles[k]) * 256 * sizeof(float4));
+    g0.recvSlabs[k].alloc((size_t)std::max(1, tiles[k]) * 256 * eb);
   }
   if (distinct) {
     const RcclApi& nc = rccl();
@@ -623,7 +675,7 @@ void Device::gather_local(int W, int H, int numTiles) {
     }
     rccl_check(nc.GroupStart(), "ncclGroupStart");
     for (int k = 1; k < N; ++k) {
-      const size_t bytes = (size_t)tiles[k] * 256 * sizeof(float4);
+      const size_t bytes = (size_t)tiles[k] * 256 * eb;
       if (!bytes) continue;
       rccl_check(nc.Send(ctx[k]->dSlab.p, bytes, ncclUint8, 0, localComms[k], ctx[k]->stream), "ncclSend");
       rccl_check(nc.Recv(g0.recvSlabs[k].p, bytes, ncclUint8, k, localComms[0], g0.stream), "ncclRecv");
@@ -632,7 +684,7 @@ void Device::gather_local(int W, int H, int numTiles) {
   } else {
     for (int k = 1; k < N; ++k) {
       HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
-      const size_t bytes = (size_t)tiles[k] * 256 * sizeof(float4);
+      const size_t bytes = (size_t)tiles[k] * 256 * eb;
       if (bytes)
         HIP_CHECK(hipMemcpyPeerAsync(g0.recvSlabs[k].p, g0.hipDevice, ctx[k]->dSlab.p, ctx[k]->hipDevice, bytes,
                                      g0.stream));
@@ -640,8 +692,8 @@ void Device::gather_local(int W, int H, int numTiles) {
   }
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   for (int k = 1; k < N; ++k)
-    launch_unpack_tiles(g0.recvSlabs[k].as<float4>(), g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H,
-                        rgb8Stride, shardIndex + k * shardCount, shardCount * N, tiles[k], g0.stream);
+    launch_unpack_tiles(g0.recvSlabs[k].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), lay[k], tiles[k],
+                        g0.stream);
   for (int k = 0; k < N; ++k) {
     HIP_CHECK(hipSetDevice(ctx[k]->hipDevice));
     HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
@@ -650,36 +702,52 @@ void Device::gather_local(int W, int H, int numTiles) {
 }
 
 // This process's tiles (shard shardIndex of shardCount, already gathered on ctx[0]) to rank 0
-// of the process communicator (yrtSetShardComm): every rank packs its tiles, rank 0 receives
-// each peer's slab (grouped RCCL send/recv) and unpacks it into its frame.
-void Device::gather_process(int W, int H, int numTiles) {
+// of the process communicator (yrtSetShardComm): the ranks first exchange their render status
+// (one 4-byte min all-reduce, so a rank whose render failed makes every rank fail instead of
+// leaving rank 0 waiting for its slab), then every rank packs its tiles and rank 0 receives
+// each peer's slab (grouped RCCL send/recv) and unpacks it into its frames.
+void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) {
   const RcclApi& nc = rccl();
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
-  const int rgb8Stride = (3 * W + 3) / 4 * 4;
   const int P = shardCount;
+  int flag = localOk ? 1 : 0;
+  dCommFlag.alloc(sizeof(int));
+  HIP_CHECK(hipMemcpyAsync(dCommFlag.p, &flag, sizeof(int), hipMemcpyHostToDevice, g0.stream));
+  rccl_check(nc.AllReduce(dCommFlag.p, dCommFlag.p, 1, ncclInt32, ncclMin, procComm, g0.stream), "ncclAllReduce");
+  HIP_CHECK(hipMemcpyAsync(&flag, dCommFlag.p, sizeof(int), hipMemcpyDeviceToHost, g0.stream));
+  HIP_CHECK(hipStreamSynchronize(g0.stream));
+  if (!flag) {
+    if (localOk) throw std::runtime_error("rtRenderFrame: a peer rank's render failed (no frame gathered)");
+    return;  // the caller rethrows this rank's own error
+  }
+  const size_t eb = slab_element_bytes(base.rgb8);
+  SlabLayout L = base;
+  L.tileStride = P;
   if (shardIndex != 0) {
+    L.tileOffset = shardIndex;
     const int tiles = shard_tiles(numTiles, shardIndex, P);
-    g0.dSlab.alloc((size_t)std::max(1, tiles) * 256 * sizeof(float4));
-    launch_pack_tiles(g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H, rgb8Stride, shardIndex, P, tiles,
-                      g0.dSlab.as<float4>(), g0.stream);
-    if (tiles) rccl_check(nc.Send(g0.dSlab.p, (size_t)tiles * 256 * sizeof(float4), ncclUint8, 0, procComm, g0.stream),
-                          "ncclSend");
+    g0.dSlab.alloc((size_t)std::max(1, tiles) * 256 * eb);
+    launch_pack_tiles(g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles, g0.dSlab.p, g0.stream);
+    if (tiles)
+      rccl_check(nc.Send(g0.dSlab.p, (size_t)tiles * 256 * eb, ncclUint8, 0, procComm, g0.stream), "ncclSend");
   } else {
     std::vector<int> tiles(P);
     for (int r = 1; r < P; ++r) {
       tiles[r] = shard_tiles(numTiles, r, P);
-      g0.recvSlabs[r].alloc((size_t)std::max(1, tiles[r]) * 256 * sizeof(float4));
+      g0.recvSlabs[r].alloc((size_t)std::max(1, tiles[r]) * 256 * eb);
     }
     rccl_check(nc.GroupStart(), "ncclGroupStart");
     for (int r = 1; r < P; ++r)
       if (tiles[r])
-        rccl_check(nc.Recv(g0.recvSlabs[r].p, (size_t)tiles[r] * 256 * sizeof(float4), ncclUint8, r, procComm,
-                           g0.stream), "ncclRecv");
+        rccl_check(nc.Recv(g0.recvSlabs[r].p, (size_t)tiles[r] * 256 * eb, ncclUint8, r, procComm, g0.stream),
+                   "ncclRecv");
     rccl_check(nc.GroupEnd(), "ncclGroupEnd");
-    for (int r = 1; r < P; ++r)
-      launch_unpack_tiles(g0.recvSlabs[r].as<float4>(), g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), W, H,
-                          rgb8Stride, r, P, tiles[r], g0.stream);
+    for (int r = 1; r < P; ++r) {
+      L.tileOffset = r;
+      launch_unpack_tiles(g0.recvSlabs[r].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles[r],
+                          g0.stream);
+    }
   }
   HIP_CHECK(hipStreamSynchronize(g0.stream));
 }
@@ -1041,7 +1109,7 @@ YRTHandle yrtNewFrameBuffer(YRTDevice dev, const char* type, size_t width, size_
   f->depth = (int)std::max<size_t>(1, buffers);
   if (ptrs) f->userPtrs.assign(ptrs, ptrs + f->depth);
   else
-    for (int i = 0; i < f->depth; ++i) f->host.emplace_back(f->stride * height, 0);
+    for (int i = 0; i < f->depth; ++i) f->host.emplace_back(new HostPixels(f->stride * height, dev->d->gpu));
   return dev->d->wrap(f);
   DEV_END(nullptr)
 }
@@ -1251,7 +1319,32 @@ int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandl
   auto F = dev->d->get<FrameBufferObj>(framebuffer, "framebuffer");
   if (!R || !C || !S || !T || !F) throw std::runtime_error("rtRenderFrame: null handle");
   if (!dev->d->gpu) throw std::runtime_error("rtRenderFrame: host-only device (created with parms \"host\")");
-  dev->d->render(*R, *C, *S, *T, *F, accumulate);
+  dev->d->render(*R, {C.get()}, *S, *T, {F.get()}, accumulate);
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtRenderFrames(YRTDevice dev, YRTHandle renderer, const YRTHandle* cameras, int numFrames, YRTHandle scene,
+                    YRTHandle tonemapper, const YRTHandle* framebuffers, int accumulate) {
+  DEV_GUARD(dev, -1)
+  if (numFrames < 1 || !cameras || !framebuffers) throw std::runtime_error("rtRenderFrames: no frames");
+  auto R = dev->d->get<RendererObj>(renderer, "renderer");
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  auto T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
+  if (!R || !S || !T) throw std::runtime_error("rtRenderFrames: null handle");
+  std::vector<std::shared_ptr<CameraObj>> cs(numFrames);
+  std::vector<std::shared_ptr<FrameBufferObj>> fs(numFrames);
+  std::vector<CameraObj*> cp(numFrames);
+  std::vector<FrameBufferObj*> fp(numFrames);
+  for (int k = 0; k < numFrames; ++k) {
+    cs[k] = dev->d->get<CameraObj>(cameras[k], "camera");
+    fs[k] = dev->d->get<FrameBufferObj>(framebuffers[k], "framebuffer");
+    if (!cs[k] || !fs[k]) throw std::runtime_error("rtRenderFrames: null camera or framebuffer handle");
+    cp[k] = cs[k].get();
+    fp[k] = fs[k].get();
+  }
+  if (!dev->d->gpu) throw std::runtime_error("rtRenderFrames: host-only device (created with parms \"host\")");
+  dev->d->render(*R, cp, *S, *T, fp, accumulate);
   return 0;
   DEV_END(-1)
 }
@@ -1503,10 +1596,25 @@ int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2) {
 int yrtSetTileShard(YRTDevice dev, int index, int count) {
   DEV_GUARD(dev, -1)
   if (count < 1 || index < 0 || index >= count) throw std::runtime_error("invalid shard");
+  // a process communicator gathers exactly its own shard (rank of world): another shard would
+  // post sends/receives its peers never match
+  if (dev->d->procComm && (index != dev->d->commRank || count != dev->d->commWorld))
+    throw std::runtime_error("yrtSetTileShard: shard differs from the process communicator's (rank " +
+                             std::to_string(dev->d->commRank) + " of " + std::to_string(dev->d->commWorld) +
+                             "); call yrtSetShardComm(dev, 0, 1, id) first to drop it");
   dev->d->shardIndex = index;
   dev->d->shardCount = count;
   return 0;
   DEV_END(-1)
+}
+
+int yrtRcclAvailable(void) {
+  try {
+    (void)rccl();
+    return 1;
+  } catch (...) {
+    return 0;
+  }
 }
 
 int yrtShardCommUniqueId(void* id128) {
@@ -1530,7 +1638,13 @@ int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128) {
   memcpy(&id, id128, sizeof(id));
   HIP_CHECK(hipSetDevice(D.hipDevice));
   if (D.procComm) rccl().CommDestroy(D.procComm), D.procComm = nullptr;
-  if (world > 1) rccl_check(rccl().CommInitRank(&D.procComm, world, id, rank), "ncclCommInitRank");
+  D.commRank = 0;
+  D.commWorld = 1;
+  if (world > 1) {
+    rccl_check(rccl().CommInitRank(&D.procComm, world, id, rank), "ncclCommInitRank");
+    D.commRank = rank;
+    D.commWorld = world;
+  }
   D.shardIndex = rank;
   D.shardCount = world;
   return 0;

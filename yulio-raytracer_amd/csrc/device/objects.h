@@ -8,6 +8,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <atomic>
 #include <map>
 #include <memory>
@@ -55,7 +58,13 @@ struct ImageObj : Object {
   int width = 0, height = 0;
   ImageFormat format = IMG_RGBA8;
   std::vector<uint8_t> data;  // width*height*4 bytes (RGBA8) or *16 (RGBAF32)
+  // process-unique identity (device caches key on it: a freed image's address can be reused)
+  const uint64_t serial = next_serial();
   ImageObj() : Object(Kind::IMAGE, "image") {}
+  static uint64_t next_serial() {
+    static std::atomic<uint64_t> n{0};
+    return ++n;
+  }
   void get(int x, int y, float c[4]) const;
 };
 
@@ -191,15 +200,36 @@ struct RendererObj : Object {
 };
 
 enum FbFormat { FB_RGB8 = 0, FB_RGBA8 = 1, FB_RGB_FLOAT32 = 2, FB_RGBA_FLOAT32 = 3 };
+// Host pixels of a framebuffer: page-locked when the device has a GPU, so the per-frame
+// write-back (a 12-face C4 cube is 85 MB of RGB8) runs at DMA speed instead of staging
+// through pageable memory; zero-filled either way.
+struct HostPixels {
+  uint8_t* p = nullptr;
+  size_t bytes = 0;
+  bool pinned = false;
+  HostPixels(size_t n, bool pin) : bytes(n) {
+    if (pin && hipHostMalloc((void**)&p, n ? n : 1, hipHostMallocDefault) == hipSuccess) pinned = true;
+    else p = (uint8_t*)malloc(n ? n : 1);
+    if (!p) throw std::bad_alloc();
+    memset(p, 0, n);
+  }
+  ~HostPixels() {
+    if (pinned) (void)hipHostFree(p);
+    else free(p);
+  }
+  HostPixels(const HostPixels&) = delete;
+  HostPixels& operator=(const HostPixels&) = delete;
+};
+
 struct FrameBufferObj : Object {
   FbFormat format = FB_RGB8;
   int width = 0, height = 0, depth = 1, cur = 0;
   size_t stride = 0;
-  std::vector<std::vector<uint8_t>> host;  // one per swapchain buffer (or user pointers)
+  std::vector<std::unique_ptr<HostPixels>> host;  // one per swapchain buffer (or user pointers)
   std::vector<void*> userPtrs;
   std::vector<float> accu;                 // AccuBuffer (x,y,z,w) per pixel
   explicit FrameBufferObj(const std::string& t) : Object(Kind::FRAMEBUFFER, t) {}
-  void* buffer(int id) { return userPtrs.size() ? userPtrs[id] : host[id].data(); }
+  void* buffer(int id) { return userPtrs.size() ? userPtrs[id] : host[id]->p; }
 };
 
 }  // namespace yrt

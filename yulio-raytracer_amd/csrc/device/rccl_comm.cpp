@@ -37,6 +37,7 @@ const RcclApi& rccl() {
     api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
     api.Send = (decltype(api.Send))sym("ncclSend");
     api.Recv = (decltype(api.Recv))sym("ncclRecv");
+    api.AllReduce = (decltype(api.AllReduce))sym("ncclAllReduce");
     api.GetErrorString = (decltype(api.GetErrorString))sym("ncclGetErrorString");
   });
   if (!err.empty()) throw std::runtime_error(err);

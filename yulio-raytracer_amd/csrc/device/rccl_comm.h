@@ -24,6 +24,7 @@ struct RcclApi {
   ncclResult_t (*GroupEnd)();
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
   const char* (*GetErrorString)(ncclResult_t);
 };
 

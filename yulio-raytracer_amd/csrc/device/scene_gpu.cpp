@@ -54,7 +54,9 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   std::vector<GpuMaterial> materials;
   std::vector<GpuTexture> textures;
   std::vector<GpuImage> images;
-  std::vector<uint8_t> texels;
+  // 8-bit images first, float images (HDRI maps) after them: the bilinear footprint records
+  // (texQuads, 4x the bytes) cover only the 8-bit part of the pool
+  std::vector<uint8_t> texels, texelsF;
   std::vector<GpuLight> lights;
   std::vector<int> envLights;
   std::map<const MaterialInst*, int> matIds;
@@ -69,10 +71,11 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     g.width = im->width;
     g.height = im->height;
     g.format = im->format;
-    size_t off = (texels.size() + 15) & ~size_t(15);
-    texels.resize(off);
-    g.offset = (int64_t)off;
-    texels.insert(texels.end(), im->data.begin(), im->data.end());
+    std::vector<uint8_t>& pool = im->format == IMG_RGBAF32 ? texelsF : texels;
+    size_t off = (pool.size() + 15) & ~size_t(15);
+    pool.resize(off);
+    g.offset = (int64_t)off;  // float images: relative to the float part until it is placed
+    pool.insert(pool.end(), im->data.begin(), im->data.end());
     images.push_back(g);
     return imgIds[im.get()] = (int)images.size() - 1;
   };
@@ -240,6 +243,16 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     S->buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return S;
   }
+  {
+    // place the float images after the 8-bit ones; image and texture records get final offsets
+    const size_t base = (texels.size() + 15) & ~size_t(15);
+    S->texels8Bytes = base;
+    texels.resize(base);
+    texels.insert(texels.end(), texelsF.begin(), texelsF.end());
+    for (GpuImage& g : images)
+      if (g.format == IMG_RGBAF32) g.offset += (int64_t)base;
+    for (GpuTexture& t : textures) t.offset = images[t.image].offset;
+  }
   for (const GpuMaterial& m : materials) S->materialMask |= 1u << m.type;
   for (const GpuLight& l : lights) S->materialMask |= 1u << (16 + l.type);  // light_bit (kernels/yrt_shade.h)
   S->nodes.upload(bvh.nodes);
@@ -258,10 +271,10 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     // bilinear footprints of the 8-bit images (kernels/yrt_shade.h tex_get): record i of an image
     // holds the 4-byte texels i, i+1, i+W, i+W+1 — the bytes the four row-major fetches read —
     // at 4x the texel's byte offset; float images keep the row-major pool only
-    std::vector<uint32_t> quads(texels.size(), 0u);
+    std::vector<uint32_t> quads(S->texels8Bytes, 0u);
     auto word = [&](size_t b) -> uint32_t {
       uint32_t w = 0;
-      if (b + 4 <= texels.size()) memcpy(&w, &texels[b], 4);
+      if (b + 4 <= S->texels8Bytes) memcpy(&w, &texels[b], 4);
       return w;
     };
     for (const GpuImage& g : images) {
@@ -365,6 +378,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   R->numGeoms = src.numGeoms;
   R->bvhDepth = src.bvhDepth;
   R->refits = src.refits;
+  R->texels8Bytes = src.texels8Bytes;
   return R;
 }
 

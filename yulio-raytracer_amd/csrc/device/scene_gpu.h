@@ -62,6 +62,7 @@ struct GpuScene {
       lights, envLights, hdriDist, media;
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)
+  size_t texels8Bytes = 0;    // the 8-bit images' part of the texel pool (float images follow it)
   // host mirrors (BVH export, precomputed light sampling, stats)
   std::vector<GpuNode> hNodes;
   std::vector<GpuTri> hTris;

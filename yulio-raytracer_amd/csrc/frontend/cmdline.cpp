@@ -580,6 +580,54 @@ void RtState::renderFprFace(size_t i) {
   for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
 }
 
+void RtState::renderCube(const std::vector<YRTHandle>& cams) {
+  if (cubeFrameBuffers.size() != cams.size() || cubeWidth != width || cubeHeight != height || cubeFormat != format) {
+    for (YRTHandle f : cubeFrameBuffers) yrtDecRef(dev, f);
+    cubeFrameBuffers.clear();
+    for (size_t k = 0; k < cams.size(); ++k)
+      cubeFrameBuffers.push_back(
+          checkH(dev, yrtNewFrameBuffer(dev, format.c_str(), width, height, 1, nullptr), "rtNewFrameBuffer"));
+    cubeWidth = width;
+    cubeHeight = height;
+    cubeFormat = format;
+  }
+  YRTHandle sc = createScene();
+  check(dev, yrtRenderFrames(dev, renderer, cams.data(), (int)cams.size(), sc, tonemapper, cubeFrameBuffers.data(), 0),
+        "rtRenderFrames");
+}
+
+std::vector<uint8_t> RtState::cubeFace(int k) {
+  const size_t bytes = fb_stride(fb_format(format), width) * height;
+  const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, cubeFrameBuffers.at(k), -1);
+  if (!p) throw std::runtime_error(std::string("rtMapFrameBuffer: ") + yrtGetLastError(dev));
+  std::vector<uint8_t> out(p, p + bytes);
+  check(dev, yrtUnmapFrameBuffer(dev, cubeFrameBuffers.at(k), -1), "rtUnmapFrameBuffer");
+  return out;
+}
+
+bool RtState::renderFprView(size_t v) {
+  if (12 * v + 12 > stereoCubeCameras.size()) throw std::runtime_error("FPR view index out of range");
+  float o0[3], o[3];
+  check(dev, yrtGetFloat3(dev, stereoCubeCameras[12 * v], "origin", &o0[0], &o0[1], &o0[2]), "rtGetFloat3");
+  for (int k = 1; k < 12; ++k) {
+    check(dev, yrtGetFloat3(dev, stereoCubeCameras[12 * v + k], "origin", &o[0], &o[1], &o[2]), "rtGetFloat3");
+    if (memcmp(o, o0, sizeof(o)) != 0) return false;
+  }
+  YRTHandle sc = createScene();
+  float up[3] = {camUp.x, camUp.y, camUp.z};
+  for (size_t j = 0; j < prims.size(); ++j)
+    check(dev, yrtUpdatePrimitive(dev, sc, j, prims[j], o0, up), "rtUpdatePrimitive");
+  check(dev, yrtCommit(dev, sc), "rtCommit(scene)");
+  std::vector<YRTHandle> cams(stereoCubeCameras.begin() + 12 * v, stereoCubeCameras.begin() + 12 * v + 12);
+  if (toeIn)  // :569-574
+    for (YRTHandle c : cams) {
+      check(dev, yrtSetBool1(dev, c, "toeIn", 1), "rtSetBool1");
+      check(dev, yrtCommit(dev, c), "rtCommit(camera)");
+    }
+  renderCube(cams);
+  return true;
+}
+
 void RtState::fprOutputMode() {
   const size_t numViews = stereoCubeCameras.size();
   if (onStage) onStage(0, (int)numViews);
@@ -596,17 +644,33 @@ void RtState::fprOutputMode() {
   std::string base = sceneFileName.substr(dir.size());
   base = base.substr(0, base.find_last_of('.'));
   std::vector<std::vector<uint8_t>> faces;
+  // whole views as one job each (renderFprView) unless YRT_FACE_LOOP=1 asks for the
+  // reference's face-by-face loop (same images)
+  const bool faceLoop = getenv("YRT_FACE_LOOP") != nullptr;
+  bool viewDone = false;
   for (size_t i = 0; i < numViews && !(stopFlag && stopFlag->load()); ++i) {
-    if (onStage) onStage((int)i, (int)numViews);
     const size_t cubeFaceIndex = i % 12;
-    if (cubeFaceIndex == 0) faces.clear();
+    if (cubeFaceIndex == 0) {
+      faces.clear();
+      viewDone = false;
+      if (!faceLoop && i + 12 <= numViews) {
+        if (onStage) onStage((int)(i / 12), (int)(numViews / 12));
+        viewDone = renderFprView(i / 12);
+        if (stopFlag && stopFlag->load()) break;
+      }
+    }
+    if (!viewDone && onStage) onStage((int)i, (int)numViews);
     char nameBuf[1024];
     int n = yrtGetString(dev, stereoCubeCameras[i], "name", nameBuf, sizeof(nameBuf));
     const std::string cameraName = n >= 0 ? std::string(nameBuf) : std::string();
-    renderFprFace(i);
-    const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
-    faces.emplace_back(p, p + stride * height);
-    check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+    if (viewDone) {
+      faces.push_back(cubeFace((int)cubeFaceIndex));
+    } else {
+      renderFprFace(i);
+      const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
+      faces.emplace_back(p, p + stride * height);
+      check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+    }
     if (waterMark && (cubeFaceIndex % 6) < 4) apply_watermark(faces.back().data(), width, height, fmt, stride);
     const std::string faceFile = dir + base + "_" + cameraName + "_" + kFaceName[cubeFaceIndex % 6] + "_image_" +
                                  (cubeFaceIndex < 6 ? "left" : "right") + ".jpg";
@@ -664,14 +728,28 @@ void RtState::outputMode(const std::string& fileName, std::vector<uint8_t>* outI
     std::vector<std::vector<uint8_t>> faces(12);
     static const char* kFaceName[6] = {"front", "right", "back", "left", "top", "bottom"};
     const std::string base = fileName.empty() ? std::string() : fileName.substr(0, fileName.find_last_of('.'));
+    // the 12 faces as one job (the scene does not change between them in this branch);
+    // YRT_FACE_LOOP=1: the reference's face-by-face loop (same images)
+    const bool faceLoop = getenv("YRT_FACE_LOOP") != nullptr;
+    if (!faceLoop) {
+      std::vector<YRTHandle> cams;
+      for (int i = 0; i < 12; ++i) cams.push_back(createCamera(i));
+      if (onStage) onStage(0, 1);
+      renderCube(cams);
+      if (stopFlag && stopFlag->load()) return;
+    }
     for (int i = 0; i < 12; ++i) {
-      if (onStage) onStage(i, 12);
-      YRTHandle cam = createCamera(i);
-      check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
-      for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
-      const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
-      faces[i].assign(p, p + stride * height);
-      check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+      if (faceLoop) {
+        if (onStage) onStage(i, 12);
+        YRTHandle cam = createCamera(i);
+        check(dev, yrtRenderFrame(dev, renderer, cam, sc, tonemapper, frameBuffer, 0), "rtRenderFrame");
+        for (int j = 0; j < numBuffers; ++j) check(dev, yrtSwapBuffers(dev, frameBuffer), "rtSwapBuffers");
+        const uint8_t* p = (const uint8_t*)yrtMapFrameBuffer(dev, frameBuffer, -1);
+        faces[i].assign(p, p + stride * height);
+        check(dev, yrtUnmapFrameBuffer(dev, frameBuffer, -1), "rtUnmapFrameBuffer");
+      } else {
+        faces[i] = cubeFace(i);
+      }
       // only the front, back and side faces carry the watermark (renderer.cpp:636-637)
       if (fprOutput && waterMark && (i % 6) < 4) apply_watermark(faces[i].data(), width, height, fmt, stride);
       if (debugging && !fileName.empty()) {

@@ -130,6 +130,21 @@ struct RtState {
   void fprOutputMode();
   // one FPR face: faceCamera update + scene commit + render (renderer.cpp:548-576)
   void renderFprFace(size_t i);
+  // The 12 faces of a stereo cube rendered as one job (yrtRenderFrames) into cubeFrameBuffers
+  // (the session framebuffer's size and format). The stereo branches render the 12 faces of
+  // a view with the same scene: the non-FPR branch never updates primitives (renderer.cpp:
+  // 742-878) and the FPR branch's per-face faceCamera update (:550-559) depends only on the
+  // camera origin, which DAELoader gives all 12 cameras of a view (ColladaLoader.cpp:483-505)
+  // — so one job gives the faces the per-face loop gives, bit for bit.
+  std::vector<YRTHandle> cubeFrameBuffers;
+  int cubeWidth = 0, cubeHeight = 0;
+  std::string cubeFormat;
+  void renderCube(const std::vector<YRTHandle>& cams);
+  // FPR view v (scene cameras 12v..12v+11): one faceCamera update + commit, then renderCube;
+  // false (nothing rendered) when the view's cameras differ in origin (per-face loop then)
+  bool renderFprView(size_t v);
+  // face k of the last renderCube as 8-bit/float pixels (session format), stride per fb_stride
+  std::vector<uint8_t> cubeFace(int k);
 };
 
 // Collada scene (collada.cpp): primitives in DAELoader order; *cameras receives the 12

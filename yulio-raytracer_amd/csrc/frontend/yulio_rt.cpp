@@ -111,6 +111,38 @@ void* yrtSessionRenderSceneCamera(YRTSession s, int i) {
   }
 }
 
+int yrtSessionRenderCube(YRTSession s) {
+  try {
+    RtState& st = s->st;
+    std::vector<YRTHandle> cams;
+    for (int i = 0; i < 12; ++i) cams.push_back(st.createCamera(i));
+    st.renderCube(cams);
+    return 0;
+  } catch (const std::exception& e) {
+    g_feError = e.what();
+    return -1;
+  }
+}
+
+int yrtSessionRenderSceneCube(YRTSession s, int view) {
+  try {
+    if (view < 0) throw std::runtime_error("FPR view index out of range");
+    if (!s->st.renderFprView((size_t)view)) throw std::runtime_error("the view's cameras differ in origin");
+    return 0;
+  } catch (const std::exception& e) {
+    g_feError = e.what();
+    return -1;
+  }
+}
+
+YRTHandle yrtSessionCubeFrameBuffer(YRTSession s, int face) {
+  if (face < 0 || (size_t)face >= s->st.cubeFrameBuffers.size()) {
+    g_feError = "no cube face framebuffer (render a cube first)";
+    return nullptr;
+  }
+  return s->st.cubeFrameBuffers[face];
+}
+
 YRTHandle yrtSessionCamera(YRTSession s, int face) {
   try {
     return s->st.createCamera(face);

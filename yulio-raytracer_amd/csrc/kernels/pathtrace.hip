@@ -210,13 +210,26 @@ __device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3
 }
 
 // ---------------------------------------------------------------- batch pixel mapping
-__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y) {
-  const int tile = bi.tileOffset + (bi.firstTile + (i >> 8)) * bi.tileStride;
+// Batch pixel i -> (frame f, pixel x, y). A batch holds whole 16x16 tiles of the job's tile
+// sequence (all frames' tiles, frame-major); the 256 pixels of a tile are consecutive, so the
+// 64 lanes of a wave (64-aligned i) always share the tile and the frame.
+__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y,
+                                            int& f) {
+  int tile = bi.tileOffset + (bi.firstTile + (i >> 8)) * bi.tileStride;
   const int within = i & 255;
-  if (tile >= rp.numTilesX * rp.numTilesY) return false;
+  f = 0;
+  if (tile >= rp.tilesPerFrame * rp.numFrames) return false;
+  if (rp.numFrames > 1) {
+    f = tile / rp.tilesPerFrame;
+    tile -= f * rp.tilesPerFrame;
+  }
   x = (tile % rp.numTilesX) * 16 + (within & 15);
   y = (tile / rp.numTilesX) * 16 + (within >> 4);
   return x < rp.width && y < rp.height;
+}
+__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y) {
+  int f;
+  return batch_pixel(rp, bi, i, x, y, f);
 }
 
 __device__ __forceinline__ float samp(const FrameView& fv, int dim, int rec) {
@@ -245,16 +258,17 @@ __global__ void k_pixel_sets(const GpuRenderParams* __restrict__ rpp, uint8_t* _
 
 __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers pb, BatchInfo bi) {
   const GpuRenderParams& rp = *fv.rp;
-  const GpuCamera& cam = *fv.cam;
   const int P = bi.numPixels * rp.spp;
   for (int base = blockIdx.x * blockDim.x; base < P; base += gridDim.x * blockDim.x) {
     const int p = base + threadIdx.x;
     bool valid = false;
     V3 org = v3s(0.f), dir = v3s(0.f);
-    if (p < P) {
+    if (p < P) {  // P and numPixels are multiples of 256: whole waves are in or out
       const int s = p / bi.numPixels, i = p - s * bi.numPixels;
-      int x, y;
-      valid = batch_pixel(rp, bi, i, x, y);
+      int x, y, f;
+      valid = batch_pixel(rp, bi, i, x, y, f);
+      // the wave's frame (one tile per wave): its camera is read with scalar loads
+      const GpuCamera& cam = fv.cam[__builtin_amdgcn_readfirstlane(f)];
       pb.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
         const int set = fv.pixelSets[(size_t)y * rp.width + x];
@@ -1295,16 +1309,17 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
                                                             float* __restrict__ fbFloat, uint8_t* __restrict__ fbRGB8,
                                                             int rgb8Stride, float4* __restrict__ accu, int accumulate) {
   const GpuRenderParams& rp = *fv.rp;
+  const size_t frameStride = (size_t)rp.width * rp.height;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < bi.numPixels; i += gridDim.x * blockDim.x) {
-    int x, y;
-    if (!batch_pixel(rp, bi, i, x, y)) continue;
+    int x, y, f;
+    if (!batch_pixel(rp, bi, i, x, y, f)) continue;
     V3 L = v3s(0.f);
     for (int s = 0; s < rp.spp; ++s) {
       const float4 l4 = pb.pathL[(size_t)s * bi.numPixels + i];
       L = L + v3(l4.x, l4.y, l4.z);
     }
     // AccuBuffer::update: non-accumulating frames store (L, spp), accumulating ones add
-    const size_t pix = (size_t)y * rp.width + x;
+    const size_t pix = (size_t)f * frameStride + (size_t)y * rp.width + x;
     float4 a = make_float4(L.x, L.y, L.z, (float)rp.spp);
     if (accumulate) {
       const float4 c = accu[pix];
@@ -1314,13 +1329,13 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
     V3 L0 = accumulate ? v3(a.x, a.y, a.z) * rcpf_(a.w) : L * rcpf_((float)rp.spp);
     if (rp.gamma != 1.0f) L0 = v3(yrt_powf(L0.x, rp.rcpGamma), yrt_powf(L0.y, rp.rcpGamma), yrt_powf(L0.z, rp.rcpGamma));
     if (fbFloat) {
-      float* o = fbFloat + ((size_t)y * rp.width + x) * 3;
+      float* o = fbFloat + pix * 3;
       o[0] = L0.x;
       o[1] = L0.y;
       o[2] = L0.z;
     }
     if (fbRGB8) {
-      uint8_t* o = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
+      uint8_t* o = fbRGB8 + ((size_t)f * rp.height + y) * rgb8Stride + 3 * x;
       o[0] = (uint8_t)clampf(L0.x * 255.0f, 0.0f, 255.0f);
       o[1] = (uint8_t)clampf(L0.y * 255.0f, 0.0f, 255.0f);
       o[2] = (uint8_t)clampf(L0.z * 255.0f, 0.0f, 255.0f);
@@ -1460,8 +1475,13 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
 #define YRT_SV_SPHERES (mat_bit(MAT_MATTE) | mat_bit(MAT_METALLIC_PAINT) | YRT_BASIC_LIGHTS)  // cornell spheres
 #define YRT_SV_STEREO \
   (mat_bit(MAT_UBER) | mat_bit(MAT_MATTE_TEXTURED) | mat_bit(MAT_METALLIC_PAINT) | YRT_BASIC_LIGHTS)  // test_stereo
+// the material types DAELoader emits (Matte default, Uber, ThinDielectric for A_ONE
+// transparency; devices/device/loaders/ColladaLoader.cpp:102,210-294): every StartRT .dae job
+#define YRT_SV_COLLADA \
+  (mat_bit(MAT_MATTE) | mat_bit(MAT_UBER) | mat_bit(MAT_THIN_DIELECTRIC) | YRT_BASIC_LIGHTS)
 #define YRT_SV_ALL (YRT_ALL_MATS | YRT_ALL_LIGHTS)
-static const unsigned kShadeVariants[] = {YRT_SV_UBER, YRT_SV_OBJ, YRT_SV_SPHERES, YRT_SV_STEREO, YRT_SV_ALL};
+static const unsigned kShadeVariants[] = {YRT_SV_UBER,   YRT_SV_OBJ,     YRT_SV_SPHERES,
+                                          YRT_SV_STEREO, YRT_SV_COLLADA, YRT_SV_ALL};
 
 template <unsigned MM>
 static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
@@ -1487,6 +1507,7 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
     case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s, countHint); break;
     case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s, countHint); break;
     case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s, countHint); break;
+    case YRT_SV_COLLADA: launch_shade_t<YRT_SV_COLLADA>(sv, fv, pb, bi, depth, s, countHint); break;
     default: launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s, countHint); break;
   }
 }
@@ -1504,64 +1525,81 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 }
 
 // ---------------------------------------------------------------- multi-GPU tile slabs
-__device__ __forceinline__ bool slab_pixel(int width, int height, int tileOffset, int tileStride, int i, int& x,
-                                           int& y) {
-  const int ntx = (width + 15) >> 4;
-  const int t = tileOffset + (i >> 8) * tileStride;
+// Slab pixel i of a shard's tile sequence -> (frame f, x, y); frames are numFrames images of
+// width x height stacked in memory, tile t = frame t / tilesPerFrame.
+__device__ __forceinline__ bool slab_pixel(const SlabLayout& L, int i, int& f, int& x, int& y) {
+  const int ntx = (L.width + 15) >> 4;
+  int t = L.tileOffset + (i >> 8) * L.tileStride;
+  f = t / L.tilesPerFrame;
+  t -= f * L.tilesPerFrame;
   x = (t % ntx) * 16 + (i & 15);
   y = (t / ntx) * 16 + ((i >> 4) & 15);
-  return x < width && y < height;
+  return x < L.width && y < L.height;
 }
 
+// rgb8: the slab holds one 32-bit word per pixel (the RGB8 bytes, what an RGB8 framebuffer
+// maps); else float4 (the float pixel, w = the RGB8 bytes)
 __global__ __launch_bounds__(256) void k_pack_tiles(const float* __restrict__ fbFloat,
-                                                    const uint8_t* __restrict__ fbRGB8, int width, int height,
-                                                    int rgb8Stride, int tileOffset, int tileStride, int n,
-                                                    float4* __restrict__ slab) {
+                                                    const uint8_t* __restrict__ fbRGB8, SlabLayout L, int n,
+                                                    void* __restrict__ slab) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int x, y;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (slab_pixel(width, height, tileOffset, tileStride, i, x, y)) {
-      const float* f = fbFloat + ((size_t)y * width + x) * 3;
-      const uint8_t* c = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
-      v = make_float4(f[0], f[1], f[2], __uint_as_float((unsigned)c[0] | ((unsigned)c[1] << 8) | ((unsigned)c[2] << 16)));
+    int f, x, y;
+    const bool in = slab_pixel(L, i, f, x, y);
+    unsigned c = 0;
+    if (in) {
+      const uint8_t* p = fbRGB8 + ((size_t)f * L.height + y) * L.rgb8Stride + 3 * x;
+      c = (unsigned)p[0] | ((unsigned)p[1] << 8) | ((unsigned)p[2] << 16);
     }
-    slab[i] = v;
+    if (L.rgb8) {
+      ((unsigned*)slab)[i] = c;
+    } else {
+      float4 v = make_float4(0.f, 0.f, 0.f, __uint_as_float(c));
+      if (in) {
+        const float* fp = fbFloat + (((size_t)f * L.height + y) * L.width + x) * 3;
+        v.x = fp[0];
+        v.y = fp[1];
+        v.z = fp[2];
+      }
+      ((float4*)slab)[i] = v;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void k_unpack_tiles(const float4* __restrict__ slab, float* __restrict__ fbFloat,
-                                                      uint8_t* __restrict__ fbRGB8, int width, int height,
-                                                      int rgb8Stride, int tileOffset, int tileStride, int n) {
+__global__ __launch_bounds__(256) void k_unpack_tiles(const void* __restrict__ slab, float* __restrict__ fbFloat,
+                                                      uint8_t* __restrict__ fbRGB8, SlabLayout L, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int x, y;
-    if (!slab_pixel(width, height, tileOffset, tileStride, i, x, y)) continue;
-    const float4 v = slab[i];
-    float* f = fbFloat + ((size_t)y * width + x) * 3;
-    f[0] = v.x;
-    f[1] = v.y;
-    f[2] = v.z;
-    const unsigned c = __float_as_uint(v.w);
-    uint8_t* o = fbRGB8 + (size_t)y * rgb8Stride + 3 * x;
+    int f, x, y;
+    if (!slab_pixel(L, i, f, x, y)) continue;
+    unsigned c;
+    if (L.rgb8) {
+      c = ((const unsigned*)slab)[i];
+    } else {
+      const float4 v = ((const float4*)slab)[i];
+      float* fp = fbFloat + (((size_t)f * L.height + y) * L.width + x) * 3;
+      fp[0] = v.x;
+      fp[1] = v.y;
+      fp[2] = v.z;
+      c = __float_as_uint(v.w);
+    }
+    uint8_t* o = fbRGB8 + ((size_t)f * L.height + y) * L.rgb8Stride + 3 * x;
     o[0] = (uint8_t)(c & 255u);
     o[1] = (uint8_t)((c >> 8) & 255u);
     o[2] = (uint8_t)((c >> 16) & 255u);
   }
 }
 
-void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, int width, int height, int rgb8Stride,
-                       int tileOffset, int tileStride, int numTiles, float4* slab, hipStream_t s) {
+void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, const SlabLayout& L, int numTiles, void* slab,
+                       hipStream_t s) {
   const int n = numTiles * 256;
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pack_tiles, dim3((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384), dim3(256), 0, s, fbFloat, fbRGB8, width,
-                     height, rgb8Stride, tileOffset, tileStride, n, slab);
+  hipLaunchKernelGGL(k_pack_tiles, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, fbFloat, fbRGB8, L, n, slab);
 }
 
-void launch_unpack_tiles(const float4* slab, float* fbFloat, uint8_t* fbRGB8, int width, int height, int rgb8Stride,
-                         int tileOffset, int tileStride, int numTiles, hipStream_t s) {
+void launch_unpack_tiles(const void* slab, float* fbFloat, uint8_t* fbRGB8, const SlabLayout& L, int numTiles,
+                         hipStream_t s) {
   const int n = numTiles * 256;
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_unpack_tiles, dim3((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384), dim3(256), 0, s, slab, fbFloat, fbRGB8,
-                     width, height, rgb8Stride, tileOffset, tileStride, n);
+  hipLaunchKernelGGL(k_unpack_tiles, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, slab, fbFloat, fbRGB8, L, n);
 }
 
 // SingleRayDevice::rtPick (api/singleray_device.cpp:692-708): one camera ray at image-plane

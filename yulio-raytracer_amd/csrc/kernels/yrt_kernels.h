@@ -43,7 +43,7 @@ struct SceneView {
 
 struct FrameView {
   const GpuRenderParams* rp;   // device copy
-  const GpuCamera* cam;        // device copy
+  const GpuCamera* cam;        // device copy: one per frame (rp->numFrames)
   const float* samples;        // [numDims][numRecords]
   const float* lightSamples;   // [numRecords][numLightSlots][8]
   const uint8_t* pixelSets;    // W*H set index per pixel
@@ -132,14 +132,21 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 int trace_profile(unsigned long long* out8, int reset);
 // Arithmetic self-check of the correctly rounded fast reciprocal (rcp_rn): see pathtrace.hip
 int check_math(int fn, unsigned long long* host2);
-// Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (image tile =
-// tileOffset + j * tileStride, j < numTiles) as a slab of numTiles * 256 float4 (rgb float,
-// w = the RGB8 bytes), in tile order j and scan order within the tile; unpack scatters a slab
-// back into the frame. Pixels outside the image are zero in the slab and skipped on unpack.
-void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, int width, int height, int rgb8Stride,
-                       int tileOffset, int tileStride, int numTiles, float4* slab, hipStream_t s);
-void launch_unpack_tiles(const float4* slab, float* fbFloat, uint8_t* fbRGB8, int width, int height, int rgb8Stride,
-                         int tileOffset, int tileStride, int numTiles, hipStream_t s);
+// Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (job tile =
+// tileOffset + j * tileStride, j < numTiles, over numFrames stacked frames of tilesPerFrame
+// tiles) as a slab of numTiles * 256 elements in tile order j and scan order within the tile;
+// unpack scatters a slab back into the frames. Elements are 32-bit RGB8 words (rgb8 = 1: the
+// framebuffer is RGB8, a quarter of the bytes) or float4 (rgb float, w = the RGB8 bytes).
+// Pixels outside the image are zero in the slab and skipped on unpack.
+struct SlabLayout {
+  int width, height, rgb8Stride, tilesPerFrame;
+  int tileOffset, tileStride, rgb8, pad;
+};
+inline size_t slab_element_bytes(int rgb8) { return rgb8 ? 4 : 16; }
+void launch_pack_tiles(const float* fbFloat, const uint8_t* fbRGB8, const SlabLayout& L, int numTiles, void* slab,
+                       hipStream_t s);
+void launch_unpack_tiles(const void* slab, float* fbFloat, uint8_t* fbRGB8, const SlabLayout& L, int numTiles,
+                         hipStream_t s);
 void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, float4* out, hipStream_t s);
 // BVH refit after faceCamera updates: rewrite triangles [firstTri, firstTri+numTris) (global
 // ids) from the vertex buffer in every leaf slot that references them (leafSlots[leafStart[g]

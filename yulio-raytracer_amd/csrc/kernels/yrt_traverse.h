@@ -1,4 +1,4 @@
-// yrt_traverse.h — BVH2 traversal + Embree-convention triangle test, device side.
+// yrt_traverse.h — 4-wide BVH traversal + Embree-convention triangle test, device side.
 //
 // Replaces Embree 2.15 rtcIntersect / rtcOccluded (call sites
 // integrators/pathtraceintegrator.cpp:72,160, renderers/debugrenderer.cpp:109).
@@ -156,13 +156,13 @@ __device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, fl
   // and the closest hit (smallest (t, triangle id)) is the same for any visit order.
   const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
   const f2 mx = {-r.oi.x, -r.oi.x}, my = {-r.oi.y, -r.oi.y}, mz = {-r.oi.z, -r.oi.z};
-#define YRT_SLAB(P, I, M, O) __builtin_elementwise_fma(P, I, M)
-  const f2 nx01 = YRT_SLAB((f2{nx.x, nx.y}), ix, mx, ox2), nx23 = YRT_SLAB((f2{nx.z, nx.w}), ix, mx, ox2);
-  const f2 fx01 = YRT_SLAB((f2{fx.x, fx.y}), ix, mx, ox2), fx23 = YRT_SLAB((f2{fx.z, fx.w}), ix, mx, ox2);
-  const f2 ny01 = YRT_SLAB((f2{ny.x, ny.y}), iy, my, oy2), ny23 = YRT_SLAB((f2{ny.z, ny.w}), iy, my, oy2);
-  const f2 fy01 = YRT_SLAB((f2{fy.x, fy.y}), iy, my, oy2), fy23 = YRT_SLAB((f2{fy.z, fy.w}), iy, my, oy2);
-  const f2 nz01 = YRT_SLAB((f2{nz.x, nz.y}), iz, mz, oz2), nz23 = YRT_SLAB((f2{nz.z, nz.w}), iz, mz, oz2);
-  const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz, oz2), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz, oz2);
+#define YRT_SLAB(P, I, M) __builtin_elementwise_fma(P, I, M)
+  const f2 nx01 = YRT_SLAB((f2{nx.x, nx.y}), ix, mx), nx23 = YRT_SLAB((f2{nx.z, nx.w}), ix, mx);
+  const f2 fx01 = YRT_SLAB((f2{fx.x, fx.y}), ix, mx), fx23 = YRT_SLAB((f2{fx.z, fx.w}), ix, mx);
+  const f2 ny01 = YRT_SLAB((f2{ny.x, ny.y}), iy, my), ny23 = YRT_SLAB((f2{ny.z, ny.w}), iy, my);
+  const f2 fy01 = YRT_SLAB((f2{fy.x, fy.y}), iy, my), fy23 = YRT_SLAB((f2{fy.z, fy.w}), iy, my);
+  const f2 nz01 = YRT_SLAB((f2{nz.x, nz.y}), iz, mz), nz23 = YRT_SLAB((f2{nz.z, nz.w}), iz, mz);
+  const f2 fz01 = YRT_SLAB((f2{fz.x, fz.y}), iz, mz), fz23 = YRT_SLAB((f2{fz.z, fz.w}), iz, mz);
 #undef YRT_SLAB
   const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
   // v_max/v_min written out (+1.5 % on C3, shadow trace 5.84 -> 5.38 ms/launch,

@@ -238,6 +238,16 @@ class Device:
         self._rc(N.dev.yrtRenderFrame(self.h, renderer, camera, scene, toneMapper, frameBuffer, int(accumulate)),
                  "rtRenderFrame")
 
+    def rtRenderFrames(self, renderer, cameras, scene, toneMapper, frameBuffers, accumulate=0):
+        """yrtRenderFrames: frame k through cameras[k] into frameBuffers[k], one wavefront job."""
+        n = len(cameras)
+        if len(frameBuffers) != n:
+            raise ValueError("one framebuffer per camera")
+        cams = (C.c_void_p * n)(*cameras)
+        fbs = (C.c_void_p * n)(*frameBuffers)
+        self._rc(N.dev.yrtRenderFrames(self.h, renderer, cams, n, scene, toneMapper, fbs, int(accumulate)),
+                 "rtRenderFrames")
+
     def rtMapFrameBuffer(self, frameBuffer, bufID=-1):
         return self._h(N.dev.yrtMapFrameBuffer(self.h, frameBuffer, bufID), "rtMapFrameBuffer")
 
@@ -356,6 +366,11 @@ class Device:
         return int(N.dev.yrtGetDeviceCount(self.h))
 
     @staticmethod
+    def rccl_available() -> bool:
+        """librccl loads (checked on every rank before the collective communicator init)."""
+        return bool(N.dev.yrtRcclAvailable())
+
+    @staticmethod
     def shard_comm_unique_id() -> bytes:
         """128-byte RCCL unique id (rank 0), to broadcast to the other ranks."""
         buf = (C.c_uint8 * 128)()
@@ -444,6 +459,30 @@ class Session:
         fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[i["framebufferFormat"]]
         N.dev.yrtUnmapFrameBuffer(self.device.h, i["framebuffer"], -1)
         return self.device.framebuffer_array(i["framebuffer"], i["width"], i["height"], fmt)
+
+    def _cube_faces(self):
+        i = self.info()
+        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[i["framebufferFormat"]]
+        out = []
+        for f in range(12):
+            fb = N.fe.yrtSessionCubeFrameBuffer(self.h, f)
+            if not fb:
+                raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+            out.append(self.device.framebuffer_array(fb, i["width"], i["height"], fmt))
+        return out
+
+    def render_cube(self, read=True):
+        """The 12 stereo cube faces as one job (yrtSessionRenderCube); list of 12 numpy images
+        (None when read=False: the faces stay in the session's framebuffers)."""
+        if N.fe.yrtSessionRenderCube(self.h) != 0:
+            raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+        return self._cube_faces() if read else None
+
+    def render_scene_cube(self, view=0, read=True):
+        """The 12 faces of FPR view `view` as one job (yrtSessionRenderSceneCube)."""
+        if N.fe.yrtSessionRenderSceneCube(self.h, int(view)) != 0:
+            raise RuntimeError(N.fe.yrtFrontendLastError().decode())
+        return self._cube_faces() if read else None
 
     def export_frame(self, face=-1, camera=None) -> bytes:
         i = self.info()

@@ -126,6 +126,7 @@ _sig(dev, "yrtSetPointer", i32, vp, vp, cstr, vp)
 _sig(dev, "yrtClear", i32, vp, vp)
 _sig(dev, "yrtCommit", i32, vp, vp)
 _sig(dev, "yrtRenderFrame", i32, vp, vp, vp, vp, vp, vp, i32)
+_sig(dev, "yrtRenderFrames", i32, vp, vp, C.POINTER(vp), i32, vp, vp, C.POINTER(vp), i32)
 _sig(dev, "yrtMapFrameBuffer", vp, vp, vp, i32)
 _sig(dev, "yrtUnmapFrameBuffer", i32, vp, vp, i32)
 _sig(dev, "yrtSwapBuffers", i32, vp, vp)
@@ -145,6 +146,7 @@ _sig(dev, "yrtSetBatchCapacity", i32, vp, C.c_int64)
 _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
 _sig(dev, "yrtShardCommUniqueId", i32, vp)
 _sig(dev, "yrtSetShardComm", i32, vp, i32, i32, vp)
+_sig(dev, "yrtRcclAvailable", i32)
 _sig(dev, "yrtGetDeviceCount", i32, vp)
 _sig(dev, "yrtSetRefitCommits", i32, vp, i32)
 _sig(dev, "yrtGetSceneRefits", i32, vp, vp)
@@ -165,6 +167,9 @@ _sig(fe, "yrtFrontendLastError", cstr)
 _sig(fe, "yrtSessionInfo", i32, vp, C.POINTER(SessionInfo))
 _sig(fe, "yrtSessionCamera", vp, vp, i32)
 _sig(fe, "yrtSessionRender", vp, vp, i32)
+_sig(fe, "yrtSessionRenderCube", i32, vp)
+_sig(fe, "yrtSessionRenderSceneCube", i32, vp, i32)
+_sig(fe, "yrtSessionCubeFrameBuffer", vp, vp, i32)
 _sig(fe, "yrtSessionNumSceneCameras", i32, vp)
 _sig(fe, "yrtSessionSceneCamera", vp, vp, i32)
 _sig(fe, "yrtSessionRenderSceneCamera", vp, vp, i32)
