@@ -228,6 +228,11 @@ YRT_API int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset);
  * reciprocal (rcp_rn, common/yrt_math.h) with the IEEE division 1.0f/x for all 2^32 inputs.
  * out2[0] = mismatches, out2[1] = the smallest mismatching input (or UINT64_MAX). */
 YRT_API int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2);
+/* Parity debugging: out4 == NULL arms the capture of the per-sample radiance (the pathL terms
+ * the resolve sums, in s order) of pixel id y*width+x (-1 disarms) of frame `frame` for the
+ * following renders (buffer of maxSamples float4); out4 != NULL copies the captured samples
+ * and returns their count. Compare with oracle_debug_pixel. */
+YRT_API int yrtDebugPixelSamples(YRTDevice dev, int pixelId, int frame, float* out4, int maxSamples);
 /* Decoder check: 8-bit pixels of a .jpg/.png in file row order (top row first), before the
  * Image4c flip/requantization of rtNewImageFromFile. Call with out=NULL to get the size. */
 YRT_API int yrtDebugDecodeImage(const char* file, int* width, int* height, int* channels, uint8_t* out,

@@ -41,6 +41,7 @@ def _sig(name, res, *args):
 
 _sig("oracle_render", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, vp, C.POINTER(OracleStats))
 _sig("oracle_trace", i32, vp, sz, vp, vp, i32, i32, vp)
+_sig("oracle_debug_pixel", i32, vp, sz, i32, i32, i32, i32, vp, i32)
 _sig("oracle_render_shard", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, i32, i32, vp,
      C.POINTER(OracleStats))
 _sig("oracle_count_visits", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
@@ -84,6 +85,15 @@ def render_shard(blob: bytes, width, height, gamma, index, count, threads=0):
     if rc != 0:
         raise RuntimeError(f"oracle_render_shard: {_err()}")
     return out, {n: getattr(st, n) for n, _ in st._fields_}
+
+
+def debug_pixel(blob: bytes, width, height, x, y, max_spp=1 << 16):
+    """Per-sample radiance of pixel (x, y): float32 (spp, 3), in the pixel's summation order."""
+    out = np.zeros((max_spp, 3), np.float32)
+    n = _lib.oracle_debug_pixel(blob, len(blob), width, height, x, y, out.ctypes.data, max_spp)
+    if n < 0:
+        raise RuntimeError(f"oracle_debug_pixel: {_err()}")
+    return out[:min(n, max_spp)]
 
 
 def trace(blob: bytes, org4: np.ndarray, dir4: np.ndarray, any_hit=False):

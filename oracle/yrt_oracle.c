@@ -307,7 +307,7 @@ typedef struct {
   V3 reflectance;                               /* Matte */
   int Kd;                                       /* texture object index, -1 */
   float s0[2], ds[2];
-  V3 shadeColor;                                /* MetallicPaint */
+  V3 shadeColor, glitterColor; float glitterSpread;  /* MetallicPaint */
   float eta;
   float d; V3 KdC, Ks; float Ns;                /* Obj */
   int map_d, map_Kd, map_Ks, map_Ns, map_Bump;
@@ -483,6 +483,8 @@ static void mat_build(const Blob* B, int oi, Material* m) {
   } else if (!strcasecmp(t, "MetallicPaint")) { /* metallicpaint.h:23-34 */
     m->type = MT_METALLIC;
     m->shadeColor = p_v3(o, "shadeColor", vs(1.0f));
+    m->glitterColor = p_v3(o, "glitterColor", vs(0.0f));
+    m->glitterSpread = p_float(o, "glitterSpread", 1.0f);
     m->eta = p_float(o, "eta", 1.4f);
   } else if (!strcasecmp(t, "Obj")) { /* obj.h:17-33 */
     m->type = MT_OBJ;
@@ -624,6 +626,34 @@ static Mesh* shape_build(const Blob* B, int oi) {
       }
     }
     m->nt = t;
+  } else if (!strcasecmp(o->type, "disk")) { /* shapes/disk.h:33-65; apex normal (0,0,1), texcoord (0,0):
+                                                 the reference reads them out of bounds (undefined) */
+    m->kind = GK_FULL;
+    const V3 P = p_v3(o, "P", vs(0.f));
+    const float h = p_float(o, "h", 0.f), r = p_float(o, "r", 0.f);
+    const int n = p_int(o, "numTriangles", 0);
+    if (n < 1) { mesh_free(m); return NULL; }
+    m->nv = n + 1;
+    m->nt = n;
+    m->pos = (V3*)malloc(sizeof(V3) * (size_t)(n + 1));
+    m->nor = (V3*)malloc(sizeof(V3) * (size_t)(n + 1));
+    m->uv = (float*)calloc(2 * (size_t)(n + 1), sizeof(float));
+    m->tri = (int*)malloc(sizeof(int) * 3 * (size_t)n);
+    const float rcpN = rcp((float)n);
+    for (int phi = 0; phi < n; phi++) {
+      const V3 d = v3(sinf((float)phi * 2.0f * PI_F * rcpN), cosf((float)phi * 2.0f * PI_F * rcpN), 0.0f);
+      m->pos[phi] = add(P, muls(d, r));
+      m->nor[phi] = v3(0.f, 0.f, 1.f);
+    }
+    m->pos[n] = add(P, v3(0.f, 0.f, h));
+    m->nor[n] = v3(0.f, 0.f, 1.f);
+    for (int phi = 0; phi < n; phi++) {
+      const int p0 = n, p1 = phi % n, p2 = (phi + 1) % n;
+      int* t = &m->tri[3 * phi];
+      if (phi % 3 == 0) { t[0] = p0; t[1] = p2; t[2] = p1; }
+      else if (phi % 3 == 1) { t[0] = p1; t[1] = p0; t[2] = p2; }
+      else { t[0] = p2; t[1] = p1; t[2] = p0; }
+    }
   } else if (!strcasecmp(o->type, "triangle")) {
     m->kind = GK_TRIANGLE;
     m->nv = 3;
@@ -1433,7 +1463,7 @@ static void post_intersect(const World* W, const Ray* r, const Hit* h, DG* dg) {
 /* ---- BRDF components (brdfs/ headers); type bits brdfs/brdf.h:10-30 */
 #define BT_DIFFUSE 0x000F000Fu
 enum { B_LAMBERT, B_DIEL_REFL, B_CONST_TRANS, B_THIN_TRANS, B_LAYER, B_MICRO, B_TRANS, B_SPEC, B_REFL, B_COND,
-       B_MICRO_COND, B_MICRO_ANISO, B_MINNAERT, B_VELVETY, B_DIEL_TRANS };
+       B_MICRO_COND, B_MICRO_ANISO, B_MINNAERT, B_VELVETY, B_DIEL_TRANS, B_LAYER_GLITTER };
 typedef struct { int kind; uint32_t type; V3 R; float a, b, c; V3 eta, k; } Brdf;
 typedef struct { int n; Brdf c[8]; } BSet;
 static void bs_add(BSet* s, int kind, uint32_t type, V3 R, float a, float b, float c) {
@@ -1542,6 +1572,31 @@ static V3 layer_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   float Fo = 1.0f - fres3(cO, cO1, c->a);
   return muls(mulv(mulv(mulv(vs(Fo), vs(1.f)), Fg), vs(1.f)), Fi);
 }
+/* MetallicPaint glitter (materials/metallicpaint.h:63-70): DielectricLayer<Microfacet<
+ * FresnelConductor(0.62, 4.8), PowerCosineDistribution(rcp(glitterSpread), Ns)>>(one, 1, eta,
+ * glitterColor); c->a = etait, c->b = etati, c->c = n. The ground is a B_MICRO_COND record. */
+static Brdf glitter_ground(const Brdf* c) {
+  Brdf g;
+  memset(&g, 0, sizeof(g));
+  g.kind = B_MICRO_COND; g.type = 0x10u; g.R = c->R; g.a = c->c;
+  g.eta = vs(0.62f); g.k = vs(4.8f);
+  return g;
+}
+static V3 glitter_layer_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) { /* dielectriclayer.h:27-38 */
+  float cO = dot(wo, dg->Ns), cI = dot(wi, dg->Ns);
+  if (cI <= 0.0f || cO <= 0.0f) return vs(0.f);
+  float cO1, cI1;
+  V3 wo1, wi1;
+  refract5(wo, dg->Ns, c->a, cO, &cO1, &wo1);
+  refract5(wi, dg->Ns, c->a, cI, &cI1, &wi1);
+  float Fi = 1.0f - fres3(cI, cI1, c->a);
+  const Brdf g = glitter_ground(c);
+  V3 Fg = micro_eval(&g, neg(wo1), dg, neg(wi1));
+  float Fo = 1.0f - fres3(cO, cO1, c->a);
+  return muls(mulv(mulv(mulv(vs(Fo), vs(1.f)), Fg), vs(1.f)), Fi);
+}
+static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3* wi, float* pdf);
+
 /* Specular::eval (brdfs/specular.h:20-24) */
 static V3 spec_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   V3 r = reflect2(wo, dg->Ns);
@@ -1557,6 +1612,7 @@ static V3 brdf_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
     case B_REFL: return c->R;
     case B_MINNAERT: return minnaert_eval(c, wo, dg, wi);
     case B_VELVETY: return velvety_eval(c, wo, dg, wi);
+    case B_LAYER_GLITTER: return glitter_layer_eval(c, wo, dg, wi);
     default: return vs(0.f);
   }
 }
@@ -1684,6 +1740,28 @@ static V3 brdf_sample(const Brdf* c, V3 wo, const DG* dg, float sx, float sy, V3
       *pdf = refract5(wo, dg->Ns, c->a, cO, &cI, wi);
       return vs(1.0f - fres3(cO, cI, c->a));
     }
+    case B_LAYER_GLITTER: { /* dielectriclayer.h:40-62 over the glitter microfacet's sample */
+      float cO = dot(wo, dg->Ns);
+      if (cO <= 0.0f) return vs(0.f);
+      float cO1;
+      V3 wo1;
+      refract5(wo, dg->Ns, c->a, cO, &cO1, &wo1);
+      const Brdf g = glitter_ground(c);
+      V3 wi1 = vs(0.f);
+      float p1 = 0.f;
+      V3 Fg = brdf_sample(&g, neg(wo1), dg, sx, sy, &wi1, &p1);
+      float cI1 = dot(wi1, dg->Ns);
+      if (cI1 <= 0.0f) return vs(0.f);
+      float cI;
+      V3 wi0;
+      float p0 = refract5(neg(wi1), neg(dg->Ns), c->b, cI1, &cI, &wi0);
+      if (p0 == 0.0f) return vs(0.f);
+      *wi = wi0;
+      *pdf = p1;
+      float Fi = 1.0f - fres3(cI, cI1, c->a);
+      float Fo = 1.0f - fres3(cO, cO1, c->a);
+      return muls(mulv(mulv(mulv(vs(Fo), vs(1.f)), Fg), vs(1.f)), Fi);
+    }
     case B_SPEC: { /* specular.h:26-28, shapesampler.h:104-121 */
       const float e = c->a;
       const float phi = TWO_PI_F * sx;
@@ -1779,6 +1857,9 @@ static void shade(const World* W, const Material* m, Medium cur, DG* dg, BSet* s
     case MT_METALLIC: /* DielectricReflection(1, eta) + DielectricLayer<Lambertian>(one, 1, eta, shadeColor) */
       bs_add(s, B_DIEL_REFL, 0x100u, vs(0.f), 1.0f * rcp(m->eta), 1.0f, 0);
       bs_add(s, B_LAYER, 0x1u, m->shadeColor, 1.0f * rcp(m->eta), m->eta * rcp(1.0f), 0);
+      if (m->glitterSpread != 0 && !v3zero(m->glitterColor)) /* metallicpaint.h:63-70 */
+        bs_add(s, B_LAYER_GLITTER, 0x10u, m->glitterColor, 1.0f * rcp(m->eta), m->eta * rcp(1.0f),
+               rcp(m->glitterSpread));
       break;
     case MT_OBJ: {
       if (m->map_Bump >= 0) {
@@ -2232,6 +2313,43 @@ int oracle_render_shard(const void* blob, size_t bytes, int width, int height, f
   world_free(&W);
   blob_free(&B);
   return 0;
+}
+
+/* Debug: the per-sample radiance Li of one pixel (the terms the pixel's sum adds in s order),
+ * out3[3*s..3*s+2] for s < spp; returns spp (or -1). */
+int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3, int maxSpp) {
+  Blob B;
+  if (blob_parse(blob, bytes, &B)) return -1;
+  World W;
+  if (world_build(&B, &W)) { blob_free(&B); return -1; }
+  RCfg R;
+  Camera C;
+  if (rcfg_build(&B, &R) || camera_build(&B, &C) || R.debug) { world_free(&W); blob_free(&B); return -1; }
+  Table T;
+  table_build(&T, R.spp, R.sets, 0, R.maxDepth, 1 + R.maxDepth, R.filter, &W);
+  uint8_t* sets = (uint8_t*)malloc((size_t)width * height);
+  oracle_pixel_sets(width, height, T.sets, sets);
+  const float rcpW = rcp((float)width), rcpH = rcp((float)height);
+  const int set = sets[(size_t)y * width + x];
+  double nc = 0, ns = 0;
+  const int spp = T.spp;
+  for (int s = 0; s < spp && s < maxSpp; s++) {
+    const int rec = set * spp + s;
+    const float fx = ((float)x + T.t[rec]) * rcpW;
+    const float fy = ((float)y + T.t[(size_t)T.rec + rec]) * rcpH;
+    Ray ray;
+    camera_ray(&C, fx, fy, T.t[(size_t)2 * T.rec + rec], T.t[(size_t)3 * T.rec + rec], &ray.org, &ray.dir);
+    ray.tnear = 0.f;
+    ray.tfar = INFINITY;
+    const V3 L = Li(&W, &R, &T, rec, ray, (uint32_t)(y * width + x), s, B.seed, fx, fy, &nc, &ns);
+    out3[3 * s] = L.x; out3[3 * s + 1] = L.y; out3[3 * s + 2] = L.z;
+  }
+  free(sets);
+  free(T.t);
+  free(T.light);
+  world_free(&W);
+  blob_free(&B);
+  return spp;
 }
 
 int oracle_trace(const void* blob, size_t bytes, const float* org4, const float* dir4, int n, int anyHit, float* hit4) {

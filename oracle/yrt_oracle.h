@@ -68,6 +68,8 @@ int oracle_render_shard(const void* blob, size_t bytes, int width, int height, f
 
 /* Traces rays against the blob's scene: org4/dir4 as in yrtIntersect; hit4 = (t,u,v,tri)
  * (tri as int bits, -1 miss). anyHit != 0 -> occluded test, hit4.w = 1/0. */
+/* Debug: per-sample radiance Li of pixel (x, y), out3[3*s..] for s < min(spp, maxSpp); returns spp. */
+int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3, int maxSpp);
 int oracle_trace(const void* blob, size_t bytes, const float* org4, const float* dir4, int n, int anyHit,
                  float* hit4);
 

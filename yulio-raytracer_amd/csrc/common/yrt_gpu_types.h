@@ -59,6 +59,7 @@ enum MaterialType : int32_t {
   MAT_METAL = 10,
   MAT_BRUSHED_METAL = 11,
   MAT_VELVET = 12,
+  MAT_METALLIC_GLITTER = 13,  // MetallicPaint with glitter (glitterSpread != 0, glitterColor != 0)
 };
 
 // Parameter slots per material type (filled by device/materials.cpp from Parms with the

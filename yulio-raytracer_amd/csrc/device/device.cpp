@@ -925,7 +925,7 @@ YRTHandle yrtNewMaterial(YRTDevice dev, const char* type) {
 
 YRTHandle yrtNewShape(YRTDevice dev, const char* type) {
   DEV_GUARD(dev, nullptr)
-  if (!ieq(type, "trianglemesh") && !ieq(type, "sphere") && !ieq(type, "triangle"))
+  if (!ieq(type, "trianglemesh") && !ieq(type, "sphere") && !ieq(type, "triangle") && !ieq(type, "disk"))
     throw std::runtime_error(std::string("shape type '") + type + "' is outside the MI355X device's scope");
   return dev->d->wrap(std::make_shared<ShapeObj>(type));
   DEV_END(nullptr)
@@ -1581,6 +1581,28 @@ int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset) {
   DEV_GUARD(dev, -1)
   HIP_CHECK(hipDeviceSynchronize());
   return trace_profile((unsigned long long*)out8, reset);
+  DEV_END(-1)
+}
+
+int yrtDebugPixelSamples(YRTDevice dev, int pixelId, int frame, float* out4, int maxSamples) {
+  DEV_GUARD(dev, -1)
+  Device& D = *dev->d;
+  if (!D.gpu) throw std::runtime_error("host-only device");
+  HIP_CHECK(hipSetDevice(D.hipDevice));
+  static DevBuf buf;  // one capture per process (a debugging aid)
+  static int capacity = 0;
+  if (!out4) {
+    if (pixelId < 0) return debug_pixel_capture(-1, -1, nullptr);
+    if (maxSamples < 1) throw std::runtime_error("yrtDebugPixelSamples: maxSamples < 1");
+    buf.alloc((size_t)maxSamples * sizeof(float4));
+    HIP_CHECK(hipMemset(buf.p, 0, (size_t)maxSamples * sizeof(float4)));
+    capacity = maxSamples;
+    return debug_pixel_capture(pixelId, frame, buf.as<float4>());
+  }
+  const int n = std::min(maxSamples, capacity);
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(out4, buf.p, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+  return n;
   DEV_END(-1)
 }
 

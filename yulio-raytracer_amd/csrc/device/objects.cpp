@@ -85,13 +85,18 @@ void MaterialObj::commit() {
     V3 glitter = parms.getV3("glitterColor", v3s(0.f));
     float glitterSpread = parms.getFloat("glitterSpread", 1.0f);
     float eta = parms.getFloat("eta", 1.4f);
-    if (glitterSpread != 0 && glitter != v3s(0.f))
-      throw std::runtime_error("MetallicPaint glitter is not supported by the MI355X device");
     p[0] = shade.x; p[1] = shade.y; p[2] = shade.z;
     p[3] = eta;
     p[4] = 1.0f * rcpf_(eta);   // DielectricReflection(1, eta): eta_ = etai*rcp(etat)
     p[5] = 1.0f * rcpf_(eta);   // DielectricLayer etait
     p[6] = eta * rcpf_(1.0f);   // DielectricLayer etati
+    // glitter flakes (metallicpaint.h:63-70): a third component, DielectricLayer<Microfacet<
+    // FresnelConductor(aluminium), PowerCosine(rcp(glitterSpread), Ns)>>(one, 1, eta, glitterColor)
+    if (glitterSpread != 0 && glitter != v3s(0.f)) {
+      m->gm.type = MAT_METALLIC_GLITTER;
+      p[7] = glitter.x; p[8] = glitter.y; p[9] = glitter.z;
+      p[10] = rcpf_(glitterSpread);
+    }
   } else if (ieq(type, "Obj")) {
     // materials/obj.h:17-33
     m->gm.type = MAT_OBJ;
@@ -303,6 +308,35 @@ void ShapeObj::commit() {
         if (theta > 1) { m->tri.push_back(p10); m->tri.push_back(p00); m->tri.push_back(p01); }
         if (theta < numTheta) { m->tri.push_back(p11); m->tri.push_back(p10); m->tri.push_back(p01); }
       }
+    }
+  } else if (ieq(type, "disk")) {
+    // shapes/disk.h:33-65: a fan of numTriangles triangles around an apex at P + (0,0,h), with
+    // alternating winding. The reference pushes numTriangles normals and texcoords for
+    // numTriangles + 1 positions, so the apex's shading normal is an out-of-bounds read of its
+    // vector (undefined); here the apex gets the normal (0,0,1) and texcoord (0,0) every other
+    // vertex has (the same substitution in oracle/yrt_oracle.c).
+    m->kind = GEOM_MESH_FULL;
+    const V3 P = parms.getV3("P");
+    const float h = parms.getFloat("h");
+    const float r = parms.getFloat("r");
+    const int n = parms.getInt("numTriangles");
+    if (n < 1) throw std::runtime_error("disk: numTriangles must be >= 1");
+    const float rcpNumTriangles = rcpf_(float(n));
+    for (int phi = 0; phi < n; phi++) {
+      const V3 d = v3(sinf(float(phi) * 2.0f * kPi * rcpNumTriangles), cosf(float(phi) * 2.0f * kPi * rcpNumTriangles), 0.0f);
+      m->pos.push_back(P + r * d);
+      m->nor.push_back(v3(0.0f, 0.0f, 1.0f));
+      m->uv.push_back(0.0f);
+      m->uv.push_back(0.0f);
+    }
+    m->pos.push_back(P + v3(0.0f, 0.0f, h));
+    m->nor.push_back(v3(0.0f, 0.0f, 1.0f));
+    m->uv.push_back(0.0f);
+    m->uv.push_back(0.0f);
+    for (int phi = 0; phi < n; phi++) {
+      const int p0 = n, p1 = phi % n, p2 = (phi + 1) % n;
+      const int w[3][3] = {{p0, p2, p1}, {p1, p0, p2}, {p2, p1, p0}};
+      for (int k = 0; k < 3; ++k) m->tri.push_back(w[phi % 3][k]);
     }
   } else if (ieq(type, "triangle")) {
     // shapes/triangle.h:19-24 (Ng is computed by transform())

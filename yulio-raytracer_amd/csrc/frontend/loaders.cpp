@@ -439,7 +439,24 @@ struct XMLLoader {
       check(dev, yrtCommit(dev, s), "rtCommit(shape)");
       prims.push_back(checkH(dev, yrtNewShapePrimitive(dev, s, mat, transforms.back().v, 0), "rtNewShapePrimitive"));
     } else if (x->name == "Disk") {
-      throw std::runtime_error(x->loc + ": Disk shapes are outside the MI355X device's scope");
+      // loadDisk (xml_loader.cpp:491-504)
+      YRTHandle mat = material(x->child("material"));
+      const yrt_v3 P = v3(x->child("position"));
+      YRTHandle s = checkH(dev, yrtNewShape(dev, "disk"), "rtNewShape");
+      XMLp r = x->child("radius"), nt = x->child("numTriangles");
+      need(r, 1, "float");
+      need(nt, 1, "int");
+      float h = 0.0f;
+      if (XMLp hx = x->childOpt("height")) {
+        need(hx, 1, "float");
+        h = F(hx, 0);
+      }
+      check(dev, yrtSetFloat3(dev, s, "P", P.x, P.y, P.z), "rtSetFloat3");
+      check(dev, yrtSetFloat1(dev, s, "r", F(r, 0)), "rtSetFloat1");
+      check(dev, yrtSetFloat1(dev, s, "h", h), "rtSetFloat1");
+      check(dev, yrtSetInt1(dev, s, "numTriangles", I(nt, 0)), "rtSetInt1");
+      check(dev, yrtCommit(dev, s), "rtCommit(shape)");
+      prims.push_back(checkH(dev, yrtNewShapePrimitive(dev, s, mat, transforms.back().v, 0), "rtNewShapePrimitive"));
     } else if (x->name == "Group") {
       for (auto& c : x->children) {
         auto p = loadScene(c);

@@ -823,6 +823,13 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[4], 1.0f);
       add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[5], m.p[6]);
       break;
+    case MAT_METALLIC_GLITTER:
+      if constexpr (!(MM & mat_bit(MAT_METALLIC_GLITTER))) break;
+      // MetallicPaint::shade (metallicpaint.h:58-71); p as above + glitterColor [7..9], n = 1/spread [10]
+      add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[4], 1.0f);
+      add_comp(bs, C_DIEL_LAYER_LAMB, BT_DIFFUSE_REFLECTION, v3(m.p[0], m.p[1], m.p[2]), m.p[5], m.p[6]);
+      add_comp(bs, C_DIEL_LAYER_GLITTER, BT_GLOSSY_REFLECTION, v3(m.p[7], m.p[8], m.p[9]), m.p[5], m.p[6], m.p[10]);
+      break;
     case MAT_OBJ: {
       if constexpr (!(MM & mat_bit(MAT_OBJ))) break;
       // p: d[0], Kd[1..3], Ks[4..6], Ns[7]; tex: map_d, map_Kd, map_Ks, map_Ns, map_Bump
@@ -1303,6 +1310,11 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, in
   }
 }
 
+// Debug capture (yrtDebugPixelSamples): the per-sample radiance of one pixel of one frame,
+// in the pixel's summation order, for parity debugging against oracle_debug_pixel.
+__device__ int g_dbgPixel[2] = {-1, -1};  // pixel id (y * width + x), frame
+__device__ float4* g_dbgOut = nullptr;
+
 // AccuBuffer::update (api/framebuffer.h:289-304) + DefaultToneMapper::eval
 // (tonemappers/defaulttonemapper.h:23-36) + FrameBufferRGB8::set (api/framebuffer.h:220-226)
 __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, PathBuffers pb, BatchInfo bi,
@@ -1318,6 +1330,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
       const float4 l4 = pb.pathL[(size_t)s * bi.numPixels + i];
       L = L + v3(l4.x, l4.y, l4.z);
     }
+    if (g_dbgPixel[0] == y * rp.width + x && g_dbgPixel[1] == f && g_dbgOut)
+      for (int s = 0; s < rp.spp; ++s) g_dbgOut[s] = pb.pathL[(size_t)s * bi.numPixels + i];
     // AccuBuffer::update: non-accumulating frames store (L, spp), accumulating ones add
     const size_t pix = (size_t)f * frameStride + (size_t)y * rp.width + x;
     float4 a = make_float4(L.x, L.y, L.z, (float)rp.spp);
@@ -1655,6 +1669,13 @@ int check_math(int fn, unsigned long long* host2) {
   }
   (void)hipFree(d);
   return rc;
+}
+
+int debug_pixel_capture(int pixelId, int frame, float4* out) {
+  const int v[2] = {pixelId, frame};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbgPixel), v, sizeof(v)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbgOut), &out, sizeof(out)) != hipSuccess) return -1;
+  return 0;
 }
 
 int trace_profile(unsigned long long* out8, int reset) {

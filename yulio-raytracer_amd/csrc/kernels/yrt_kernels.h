@@ -130,6 +130,9 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
 int trace_profile(unsigned long long* out8, int reset);
+// Debug capture: per-sample radiance of pixel id (y * width + x) of frame `frame` written to
+// out[s] by the next resolves (pixelId -1: off)
+int debug_pixel_capture(int pixelId, int frame, float4* out);
 // Arithmetic self-check of the correctly rounded fast reciprocal (rcp_rn): see pathtrace.hip
 int check_math(int fn, unsigned long long* host2);
 // Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (job tile =

@@ -50,6 +50,8 @@ enum CompKind : int {
   C_MINNAERT = 12,        // Minnaert(R, b)                              a=b
   C_VELVETY = 13,         // Velvety(R, f)                               a=f
   C_DIEL_TRANS = 14,      // DielectricTransmission(etai, etat)          a=eta_
+  C_DIEL_LAYER_GLITTER = 15,  // DielectricLayer<Microfacet<FresnelConductor(Al),PowerCosine(n,Ns)>>
+                              // (T=1, etait, etati, glitterColor)           R, a=etait, b=etati, c=n
 };
 
 // Material-set specialization: the shade kernel is instantiated for a bitmask of material
@@ -68,9 +70,10 @@ __host__ __device__ constexpr unsigned comps_of(unsigned mats) {
          ((mats & mat_bit(9)) ? comp_bit(8) : 0u) |                                                 // Mirror
          ((mats & mat_bit(10)) ? (comp_bit(9) | comp_bit(10)) : 0u) |                               // Metal
          ((mats & mat_bit(11)) ? (comp_bit(9) | comp_bit(11)) : 0u) |                               // BrushedMetal
-         ((mats & mat_bit(12)) ? (comp_bit(12) | comp_bit(13)) : 0u);                               // Velvet
+         ((mats & mat_bit(12)) ? (comp_bit(12) | comp_bit(13)) : 0u) |                              // Velvet
+         ((mats & mat_bit(13)) ? (comp_bit(1) | comp_bit(4) | comp_bit(15)) : 0u);                  // MetallicPaint+glitter
 }
-#define YRT_ALL_MATS 0x1FFEu
+#define YRT_ALL_MATS 0x3FFEu
 // Light types ride in bits 16.. of the same instantiation mask (bit 16 + LIGHT_x).
 __host__ __device__ constexpr unsigned light_bit(int t) { return 1u << (16 + t); }
 #define YRT_BASIC_LIGHTS (light_bit(0) | light_bit(1) | light_bit(2))  // ambient, triangle, HDRI
@@ -320,6 +323,38 @@ __device__ __forceinline__ V3 microfacet_eval(const Comp& c, const GpuMaterial* 
   return c.R * D * G * F * rcpf_(4.0f * cosThetaO);
 }
 
+// The glitter flakes of MetallicPaint (materials/metallicpaint.h:63-70): Microfacet<
+// FresnelConductor(eta 0.62, k 4.8: aluminium), PowerCosineDistribution(n, Ns)> with
+// reflectivity glitterColor — microfacet.h:28-41 with the constant conductor Fresnel term.
+__device__ __forceinline__ V3 glitter_ground_eval(V3 R, float n, V3 wo, const DG& dg, V3 wi) {
+  if (dot(wi, dg.Ng) <= 0) return v3s(0.0f);
+  const float cosThetaO = dot(wo, dg.Ns);
+  const float cosThetaI = dot(wi, dg.Ns);
+  if (cosThetaI <= 0.0f || cosThetaO <= 0.0f) return v3s(0.0f);
+  const V3 wh = normalize(wi + wo);
+  const float cosThetaH = dot(wh, dg.Ns);
+  const float cosTheta = dot(wi, wh);
+  const V3 F = fresnel_conductor(cosTheta, v3s(0.62f), v3s(4.8f));
+  const float D = (n + 2) * kOneOverTwoPi * yrt_powf(fabsf(dot(wh, dg.Ns)), n);
+  const float G = fminf(fminf(1.0f, 2.0f * cosThetaH * cosThetaO * rcpf_(cosTheta)),
+                        2.0f * cosThetaH * cosThetaI * rcpf_(cosTheta));
+  return R * D * G * F * rcpf_(4.0f * cosThetaO);
+}
+// DielectricLayer<MicrofacetGlitter>::eval (brdfs/dielectriclayer.h:27-38), T = one
+__device__ __forceinline__ V3 glitter_layer_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
+  float cosThetaO = dot(wo, dg.Ns);
+  float cosThetaI = dot(wi, dg.Ns);
+  if (cosThetaI <= 0.0f || cosThetaO <= 0.0f) return v3s(0.0f);
+  float cosThetaO1, cosThetaI1;
+  V3 wo1, wi1;
+  refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaO1, wo1);
+  refract5(wi, dg.Ns, c.a, cosThetaI, cosThetaI1, wi1);
+  float Fi = 1.0f - fresnel3(cosThetaI, cosThetaI1, c.a);
+  V3 Fg = glitter_ground_eval(c.R, c.c, -wo1, dg, -wi1);
+  float Fo = 1.0f - fresnel3(cosThetaO, cosThetaO1, c.a);
+  return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
+}
+
 // Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26)
 __device__ __forceinline__ V3 minnaert_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   const float cosThetaI = clampf(dot(wi, dg.Ns));
@@ -370,6 +405,7 @@ __device__ __forceinline__ V3 comp_eval(const Comp c, const GpuMaterial* __restr
     case C_REFLECTION: YRT_IF(C_REFLECTION) return c.R; break;  // Reflection::eval (reflection.h:16-18)
     case C_MINNAERT: YRT_IF(C_MINNAERT) return minnaert_eval(c, wo, dg, wi); break;
     case C_VELVETY: YRT_IF(C_VELVETY) return velvety_eval(c, wo, dg, wi); break;
+    case C_DIEL_LAYER_GLITTER: YRT_IF(C_DIEL_LAYER_GLITTER) return glitter_layer_eval(c, wo, dg, wi); break;
     default: break;
   }
   return v3s(0.0f);
@@ -528,6 +564,46 @@ __device__ __forceinline__ V3 comp_sample(const Comp c, const GpuMaterial* __res
       wi = -wo;
       pdf = 1.0f;
       return c.R;
+    }
+    case C_DIEL_LAYER_GLITTER: {
+      YRT_IF_NOT(C_DIEL_LAYER_GLITTER) break;
+      // DielectricLayer::sample (dielectriclayer.h:40-62) over Microfacet::sample
+      // (microfacet.h:43-50) with PowerCosineDistribution::sample (power_cosine_distribution.h:27-35)
+      pdf = 0.0f;
+      float cosThetaO = dot(wo, dg.Ns);
+      if (cosThetaO <= 0.0f) return v3s(0.0f);
+      float cosThetaO1;
+      V3 wo1;
+      refract5(wo, dg.Ns, c.a, cosThetaO, cosThetaO1, wo1);
+      const V3 gwo = -wo1;
+      V3 wi1 = v3s(0.0f);
+      float pdf1 = 0.0f;
+      V3 Fg = v3s(0.0f);
+      if (dot(gwo, dg.Ns) > 0.0f) {
+        const float n = c.c;
+        const float norm1 = (n + 1) * kOneOverTwoPi;
+        const float phi = kTwoPi * sx;
+        const float cosPhi = yrt_cosf(phi);
+        const float sinPhi = yrt_sinf(phi);
+        const float cosTheta = yrt_powf(sy, rcpf_(n + 1));
+        const float sinTheta = cos2sin(cosTheta);
+        const V3 wh = mul(dg_F(dg), v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+        const float whpdf = norm1 * yrt_powf(cosTheta, n);
+        wi1 = reflect2(gwo, wh);
+        pdf1 = whpdf * rcpf_(4.0f * fabsf(dot(gwo, wh)));
+        if (dot(wi1, dg.Ns) > 0.0f) Fg = glitter_ground_eval(c.R, n, gwo, dg, wi1);
+      }
+      float cosThetaI1 = dot(wi1, dg.Ns);
+      if (cosThetaI1 <= 0.0f) return v3s(0.0f);
+      float cosThetaI;
+      V3 wi0;
+      float pdf0 = refract5(-wi1, -dg.Ns, c.b, cosThetaI1, cosThetaI, wi0);
+      if (pdf0 == 0.0f) return v3s(0.0f);
+      wi = wi0;
+      pdf = pdf1;
+      float Fi = 1.0f - fresnel3(cosThetaI, cosThetaI1, c.a);
+      float Fo = 1.0f - fresnel3(cosThetaO, cosThetaO1, c.a);
+      return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
     }
     case C_SPECULAR: {
       YRT_IF_NOT(C_SPECULAR) break;

@@ -350,6 +350,19 @@ class Device:
         N.dev.yrtGetCapturedRays(self.h, int(shadow), depth, org.ctypes.data, dir_.ctypes.data, m, C.byref(tot))
         return org, dir_, tot.value
 
+    def debug_pixel_arm(self, x, y, width, frame=0, max_samples=1 << 16):
+        """Capture the per-sample radiance of pixel (x, y) of frame `frame` in later renders."""
+        self._rc(N.dev.yrtDebugPixelSamples(self.h, int(y * width + x) if x >= 0 else -1, int(frame), None,
+                                            int(max_samples)), "debug_pixel_arm")
+
+    def debug_pixel_samples(self, spp):
+        """The captured per-sample radiance: float32 (spp, 3)."""
+        out = np.zeros((spp, 4), np.float32)
+        n = N.dev.yrtDebugPixelSamples(self.h, 0, 0, out.ctypes.data, int(spp))
+        if n < 0:
+            raise RuntimeError(f"debug_pixel_samples: {self.error()}")
+        return out[:n, :3]
+
     def set_refit_commits(self, on=True):
         self._rc(N.dev.yrtSetRefitCommits(self.h, int(on)), "set_refit_commits")
 
