@@ -329,6 +329,8 @@ typedef struct {
   int* tri;
   int cull;
   V3 Ng;
+  V3* mot;             /* per-vertex motion (TriangleMeshFull "motions", Sphere dPdt), NULL if none */
+  V3 *tanX, *tanY;     /* per-vertex tangents ("tangent_x", "tangent_y"), NULL if none */
 } Mesh;
 
 enum { LT_AMBIENT = 0, LT_TRIANGLE = 1, LT_HDRI = 2, LT_POINT = 3, LT_SPOT = 4, LT_DIRECTIONAL = 5, LT_DISTANT = 6 };
@@ -367,6 +369,7 @@ typedef struct {
   float* tv;      /* 9 floats per tri: v0 v1 v2 */
   uint32_t* tflags;
   V3 *te0, *te1, *te2;  /* v0, e1=v0-v1, e2=v2-v0 */
+  V3 *tm;               /* 3 motion vectors per tri (NULL: no moving geometry in the scene) */
   BNode* nodes; int nnodes;
   int* order;
 } World;
@@ -555,7 +558,7 @@ static void mat_build(const Blob* B, int oi, Material* m) {
 static Mesh* mesh_new(void) { return (Mesh*)calloc(1, sizeof(Mesh)); }
 static void mesh_free(Mesh* m) {
   if (!m) return;
-  free(m->pos); free(m->nor); free(m->uv); free(m->tri); free(m);
+  free(m->pos); free(m->nor); free(m->uv); free(m->tri); free(m->mot); free(m->tanX); free(m->tanY); free(m);
 }
 
 static Mesh* shape_build(const Blob* B, int oi) {
@@ -563,8 +566,9 @@ static Mesh* shape_build(const Blob* B, int oi) {
   Mesh* m = mesh_new();
   if (!strcasecmp(o->type, "trianglemesh")) { /* shapes/trianglemesh.h:14-26 */
     const Parm *pos = pfind(o, "positions"), *nor = pfind(o, "normals"), *tc = pfind(o, "texcoords"),
-               *tc0 = pfind(o, "texcoords0"), *idx = pfind(o, "indices");
-    const int withNormals = pos && nor && !tc && !tc0;
+               *tc0 = pfind(o, "texcoords0"), *idx = pfind(o, "indices"), *mot = pfind(o, "motions"),
+               *tx = pfind(o, "tangent_x"), *ty = pfind(o, "tangent_y");
+    const int withNormals = pos && !mot && nor && !tx && !ty && !tc && !tc0;
     m->kind = withNormals ? GK_NORMALS : GK_FULL;
     if (pos) {
       m->nv = (int)pos->count;
@@ -576,6 +580,17 @@ static Mesh* shape_build(const Blob* B, int oi) {
       for (uint32_t i = 0; i < nor->count; ++i) memcpy(&m->nor[i], nor->data + (size_t)i * nor->esize, 12);
       if (withNormals) m->nv = (int)nor->count; /* vertices.resize(normals) */
     }
+    /* per-vertex vec3 arrays read at vertex count (a shorter array is an out-of-bounds read in
+     * the reference; the device rejects it, so a blob never carries one) */
+#define RD3(P, DST)                                                                   \
+    if (P) {                                                                          \
+      DST = (V3*)calloc((size_t)(m->nv > (int)(P)->count ? m->nv : (int)(P)->count) + 1, sizeof(V3)); \
+      for (uint32_t i = 0; i < (P)->count; ++i) memcpy(&DST[i], (P)->data + (size_t)i * (P)->esize, 12); \
+    }
+    RD3(mot, m->mot)
+    RD3(tx, m->tanX)
+    RD3(ty, m->tanY)
+#undef RD3
     const Parm* t = tc0 ? tc0 : tc;
     if (t) {
       m->uv = (float*)malloc(sizeof(float) * 2 * (t->count ? t->count : 1));
@@ -592,7 +607,12 @@ static Mesh* shape_build(const Blob* B, int oi) {
     const V3 P = p_v3(o, "P", vs(0.f));
     const float r = p_float(o, "r", 0.f);
     const int numTheta = p_int(o, "numTheta", 0), numPhi = p_int(o, "numPhi", 0);
+    const V3 dPdt = p_v3(o, "dPdt", vs(0.f));
     m->nv = (numTheta + 1) * numPhi;
+    if (!v3zero(dPdt)) { /* sphere.h:67: one motion vector per vertex */
+      m->mot = (V3*)malloc(sizeof(V3) * (m->nv ? m->nv : 1));
+      for (int i = 0; i < m->nv; ++i) m->mot[i] = dPdt;
+    }
     m->pos = (V3*)malloc(sizeof(V3) * (m->nv ? m->nv : 1));
     m->nor = (V3*)malloc(sizeof(V3) * (m->nv ? m->nv : 1));
     m->uv = (float*)malloc(sizeof(float) * 2 * (m->nv ? m->nv : 1));
@@ -700,6 +720,15 @@ static Mesh* mesh_transform(const Mesh* s, A3 x) {
   }
   m->tri = (int*)malloc(sizeof(int) * 3 * (s->nt ? s->nt : 1));
   memcpy(m->tri, s->tri, sizeof(int) * 3 * s->nt);
+  V3** vecs[3] = {&m->mot, &m->tanX, &m->tanY};
+  const V3* src[3] = {s->mot, s->tanX, s->tanY};
+  for (int k = 0; k < 3; ++k) {
+    *vecs[k] = NULL;
+    if (src[k]) {
+      *vecs[k] = (V3*)malloc(sizeof(V3) * (s->nv ? s->nv : 1));
+      memcpy(*vecs[k], src[k], sizeof(V3) * s->nv);
+    }
+  }
   if (s->kind == GK_TRIANGLE) {
     for (int i = 0; i < 3; ++i) m->pos[i] = xfmPoint(x, s->pos[i]);
     m->Ng = normalize(cross(sub(m->pos[2], m->pos[0]), sub(m->pos[1], m->pos[0])));
@@ -709,6 +738,10 @@ static Mesh* mesh_transform(const Mesh* s, A3 x) {
   for (int i = 0; i < m->nv; ++i) m->pos[i] = xfmPoint(x, s->pos[i]);
   if (m->nor)
     for (int i = 0; i < m->nv; ++i) m->nor[i] = xfmNormal(x, s->nor[i]);
+  /* trianglemesh_full.cpp:79-85: motions and tangents are vectors */
+  for (int k = 0; k < 3; ++k)
+    if (*vecs[k])
+      for (int i = 0; i < m->nv; ++i) (*vecs[k])[i] = xfmVector(x, src[k][i]);
   return m;
 }
 
@@ -785,6 +818,21 @@ static int light_build(const Blob* B, int oi, A3 xfm, int illum, int shadow, Lig
 }
 
 /* ---------------------------------------------------------------- oracle BVH (median split) */
+/* bounds of triangle i over the frame time [0,1]: its vertices at t = 0 and t = 1 (p + m),
+ * as the reference's extract() bounds motion meshes (trianglemesh_full.cpp:152-166) */
+static void tri_box(const World* W, int i, float lo[3], float hi[3]) {
+  const float* t = &W->tv[(size_t)i * 9];
+  for (int k = 0; k < 3; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+  for (int v = 0; v < 3; ++v) {
+    const float p[3] = {t[3 * v], t[3 * v + 1], t[3 * v + 2]};
+    for (int k = 0; k < 3; ++k) { lo[k] = fminf(lo[k], p[k]); hi[k] = fmaxf(hi[k], p[k]); }
+    if (W->tm) {
+      const V3 m = W->tm[(size_t)i * 3 + v];
+      const float q[3] = {p[0] + m.x, p[1] + m.y, p[2] + m.z};
+      for (int k = 0; k < 3; ++k) { lo[k] = fminf(lo[k], q[k]); hi[k] = fmaxf(hi[k], q[k]); }
+    }
+  }
+}
 typedef struct { World* W; int* idx; float* cen; } BuildCtx;
 static int cmp_axis;
 static const float* cmp_cen;
@@ -799,12 +847,12 @@ static int bvh_rec(World* W, int* idx, const float* cen, int b, int e) {
   BNode* n = &W->nodes[ni];
   for (int k = 0; k < 3; ++k) { n->lo[k] = INFINITY; n->hi[k] = -INFINITY; }
   for (int i = b; i < e; ++i) {
-    const float* t = &W->tv[(size_t)idx[i] * 9];
-    for (int v = 0; v < 3; ++v)
-      for (int k = 0; k < 3; ++k) {
-        n->lo[k] = fminf(n->lo[k], t[3 * v + k]);
-        n->hi[k] = fmaxf(n->hi[k], t[3 * v + k]);
-      }
+    float lo[3], hi[3];
+    tri_box(W, idx[i], lo, hi);
+    for (int k = 0; k < 3; ++k) {
+      n->lo[k] = fminf(n->lo[k], lo[k]);
+      n->hi[k] = fmaxf(n->hi[k], hi[k]);
+    }
   }
   if (e - b <= 4) {
     n->left = -1 - b;
@@ -837,11 +885,9 @@ static void bvh_build_oracle(World* W) {
   float* cen = (float*)malloc(sizeof(float) * 3 * (W->ntris ? W->ntris : 1));
   for (int i = 0; i < W->ntris; ++i) {
     W->order[i] = i;
-    for (int k = 0; k < 3; ++k) {
-      const float* t = &W->tv[(size_t)i * 9];
-      float lo = fminf(fminf(t[k], t[3 + k]), t[6 + k]), hi = fmaxf(fmaxf(t[k], t[3 + k]), t[6 + k]);
-      cen[i * 3 + k] = 0.5f * (lo + hi);
-    }
+    float lo[3], hi[3];
+    tri_box(W, i, lo, hi);
+    for (int k = 0; k < 3; ++k) cen[i * 3 + k] = 0.5f * (lo[k] + hi[k]);
   }
   if (W->ntris) bvh_rec(W, W->order, cen, 0, W->ntris);
   free(cen);
@@ -850,7 +896,7 @@ static void bvh_build_oracle(World* W) {
 /* ---------------------------------------------------------------- ray / hit
  * Embree-convention Moeller-Trumbore (lights/trianglelight.h:55-65) with the cull filter
  * (trianglemesh_full.cpp:86-106); closest = smallest (t, gid). */
-typedef struct { V3 org, dir; float tnear, tfar; } Ray;
+typedef struct { V3 org, dir; float tnear, tfar, time; } Ray;
 typedef struct { float t, u, v; int tri; } Hit;
 
 static inline int tri_test(V3 v0, V3 e1, V3 e2, uint32_t flags, const Ray* r, float tfar, float* t, float* u,
@@ -900,13 +946,22 @@ static Hit trace(const World* W, const Ray* r, int any) {
       for (int i = first; i < first + n->right; ++i) {
         const int g = W->order[i];
         float t, u, v;
-        int ok = tri_test(W->te0[g], W->te1[g], W->te2[g], W->tflags[g], r, any ? r->tfar : best.t, &t, &u, &v);
+        V3 v0 = W->te0[g], e1 = W->te1[g], e2 = W->te2[g];
+        if (W->tm) { /* the triangle at the ray's time: p += time * motion (trianglemesh_full.cpp:104-109) */
+          const float* tv = &W->tv[(size_t)g * 9];
+          const V3* m = &W->tm[(size_t)g * 3];
+          const V3 p0 = add(v3(tv[0], tv[1], tv[2]), muls(m[0], r->time));
+          const V3 p1 = add(v3(tv[3], tv[4], tv[5]), muls(m[1], r->time));
+          const V3 p2 = add(v3(tv[6], tv[7], tv[8]), muls(m[2], r->time));
+          v0 = p0; e1 = sub(p0, p1); e2 = sub(p2, p0);
+        }
+        int ok = tri_test(v0, e1, e2, W->tflags[g], r, any ? r->tfar : best.t, &t, &u, &v);
         if (any) {
           if (ok) { best.t = t; best.u = u; best.v = v; best.tri = g; return best; }
         } else {
           if (!ok && best.tri >= 0 && t == best.t && g < best.tri) {
             float t2, u2, v2;
-            ok = tri_test(W->te0[g], W->te1[g], W->te2[g], W->tflags[g], r, r->tfar, &t2, &u2, &v2);
+            ok = tri_test(v0, e1, e2, W->tflags[g], r, r->tfar, &t2, &u2, &v2);
           }
           if (ok) { best.t = t; best.u = u; best.v = v; best.tri = g; }
         }
@@ -928,7 +983,7 @@ static void world_free(World* W) {
     free(W->lights[i].ycdf); free(W->lights[i].ypdf); free(W->lights[i].xcdf); free(W->lights[i].xpdf);
   }
   free(W->mats); free(W->geoms); free(W->lights); free(W->env); free(W->triGeom); free(W->tv); free(W->tflags);
-  free(W->te0); free(W->te1); free(W->te2); free(W->nodes); free(W->order);
+  free(W->te0); free(W->te1); free(W->te2); free(W->tm); free(W->nodes); free(W->order);
 }
 
 static int world_build(const Blob* B, World* W) {
@@ -993,6 +1048,9 @@ static int world_build(const Blob* B, World* W) {
   W->te0 = (V3*)malloc(sizeof(V3) * nt);
   W->te1 = (V3*)malloc(sizeof(V3) * nt);
   W->te2 = (V3*)malloc(sizeof(V3) * nt);
+  int anyMotion = 0;
+  for (int gi = 0; gi < W->ngeoms; ++gi) anyMotion |= W->geoms[gi].mesh->mot != NULL;
+  W->tm = anyMotion ? (V3*)calloc((size_t)3 * nt, sizeof(V3)) : NULL;
   for (int gi = 0; gi < W->ngeoms; ++gi) {
     const Mesh* m = W->geoms[gi].mesh;
     for (int t = 0; t < m->nt; ++t) {
@@ -1005,6 +1063,8 @@ static int world_build(const Blob* B, World* W) {
       W->te0[id] = a;
       W->te1[id] = sub(a, b);
       W->te2[id] = sub(c, a);
+      if (W->tm && m->mot)
+        for (int k = 0; k < 3; ++k) W->tm[(size_t)id * 3 + k] = m->mot[m->tri[3 * t + k]];
     }
   }
   bvh_build_oracle(W);
@@ -1419,7 +1479,12 @@ static void post_intersect(const World* W, const Ray* r, const Hit* h, DG* dg) {
     dg->s = u; dg->t = v;
   } else {
     const int i0 = m->tri[3 * prim], i1 = m->tri[3 * prim + 1], i2 = m->tri[3 * prim + 2];
-    const V3 p0 = m->pos[i0], p1 = m->pos[i1], p2 = m->pos[i2];
+    V3 p0 = m->pos[i0], p1 = m->pos[i1], p2 = m->pos[i2];
+    if (m->mot) { /* trianglemesh_full.cpp:211-215 */
+      p0 = add(p0, muls(m->mot[i0], r->time));
+      p1 = add(p1, muls(m->mot[i1], r->time));
+      p2 = add(p2, muls(m->mot[i2], r->time));
+    }
     const V3 dPdu = sub(p1, p0), dPdv = sub(p2, p0);
     dg->Ng = normalize(cross(sub(p0, p1), sub(p2, p0)));
     if (m->kind == GK_NORMALS) {
@@ -1451,10 +1516,19 @@ static void post_intersect(const World* W, const Ray* r, const Hit* h, DG* dg) {
       } else {
         dg->Ns = dg->Ng;
       }
-      const V3 dPds = normalize(sub(muls(dPdu, dtdv), muls(dPdv, dtdu)));
-      dg->Tx = normalize(sub(dPds, muls(dg->Ns, dot(dPds, dg->Ns))));
-      const V3 dPdt = normalize(sub(muls(dPdv, dsdu), muls(dPdu, dsdv)));
-      dg->Ty = normalize(sub(dPdt, muls(dg->Ns, dot(dPdt, dg->Ns))));
+      /* trianglemesh_full.cpp:244-263: interpolated tangents when given, else from dP/dst */
+      if (m->tanX) {
+        dg->Tx = add(add(muls(m->tanX[i0], w), muls(m->tanX[i1], u)), muls(m->tanX[i2], v));
+      } else {
+        const V3 dPds = normalize(sub(muls(dPdu, dtdv), muls(dPdv, dtdu)));
+        dg->Tx = normalize(sub(dPds, muls(dg->Ns, dot(dPds, dg->Ns))));
+      }
+      if (m->tanY) {
+        dg->Ty = add(add(muls(m->tanY[i0], w), muls(m->tanY[i1], u)), muls(m->tanY[i2], v));
+      } else {
+        const V3 dPdt = normalize(sub(muls(dPdv, dsdu), muls(dPdu, dsdv)));
+        dg->Ty = normalize(sub(dPdt, muls(dg->Ns, dot(dPdt, dg->Ns))));
+      }
     }
   }
   dg->error = fmaxf(fabsf(t), fmax3(absv(dg->P)));
@@ -2066,7 +2140,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
         float tMax = R->tMaxShadowRay + jl;
         const float dp = dot(wi, R->up);
         if (dp <= 0.f) tMax += R->tMaxShadowRay * 100.f * smoothstep_(0.f, 1.f, fabsf(dp));
-        Ray sr = {dg.P, wi, dg.error * R->epsilon, tMax - dg.error * R->epsilon};
+        Ray sr = {dg.P, wi, dg.error * R->epsilon, tMax - dg.error * R->epsilon, ray.time}; /* lastRay.time (:158) */
         Hit sh = trace(W, &sr, 1);
         *nShadow += 1;
         if (sh.tri >= 0) continue;
@@ -2180,6 +2254,7 @@ static void* worker(void* arg) {
                      &ray.dir); /* sample.getLens() */
           ray.tnear = 0.f;
           ray.tfar = INFINITY;
+          ray.time = J->T->t[(size_t)4 * J->T->rec + rec]; /* primary.time = sample.getTime() (:159) */
           L = add(L, Li(J->W, J->R, J->T, rec, ray, (uint32_t)(y * J->width + x), s, J->seed, fx, fy, &nc, &ns));
         }
         /* AccuBuffer::update + DefaultToneMapper::eval */
@@ -2221,6 +2296,7 @@ static void debug_render(const World* W, const RCfg* R, const Camera* C, int wid
           camera_ray(C, fx, fy, 0.f, 0.f, &ray.org, &ray.dir);
           ray.tnear = 0.f;
           ray.tfar = INFINITY;
+          ray.time = 0.f; /* the debug renderer's rays keep Ray's default time (ray.h:33) */
           int id0 = -1, id1 = -1;
           for (int depth = 0; depth < R->maxDepth; depth++) {
             Hit h = trace(W, &ray, 0);
@@ -2341,6 +2417,7 @@ int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, in
     camera_ray(&C, fx, fy, T.t[(size_t)2 * T.rec + rec], T.t[(size_t)3 * T.rec + rec], &ray.org, &ray.dir);
     ray.tnear = 0.f;
     ray.tfar = INFINITY;
+    ray.time = T.t[(size_t)4 * T.rec + rec];
     const V3 L = Li(&W, &R, &T, rec, ray, (uint32_t)(y * width + x), s, B.seed, fx, fy, &nc, &ns);
     out3[3 * s] = L.x; out3[3 * s + 1] = L.y; out3[3 * s + 2] = L.z;
   }

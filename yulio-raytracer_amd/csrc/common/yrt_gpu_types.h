@@ -23,7 +23,8 @@
 namespace yrt {
 
 enum GeomKind : int32_t { GEOM_MESH_FULL = 0, GEOM_MESH_NORMALS = 1, GEOM_TRIANGLE = 2 };
-enum GeomFlags : int32_t { GF_NORMALS = 1, GF_TEXCOORDS = 2, GF_CULL = 4 };
+enum GeomFlags : int32_t { GF_NORMALS = 1, GF_TEXCOORDS = 2, GF_CULL = 4, GF_MOTION = 8, GF_TANGENT_X = 16,
+                           GF_TANGENT_Y = 32 };
 
 struct GpuNode {
   float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];  // per child
@@ -38,6 +39,16 @@ struct GpuTri {
   float e2[4];  // xyz, w unused
 };
 static_assert(sizeof(GpuTri) == 48, "tri record size");
+
+// Moving triangles (motion blur, scenes with "motions" / Sphere dPdt): per leaf slot, beside
+// its GpuTri (which holds the t = 0 triangle), the other two vertices and the three vertices'
+// motion vectors; the triangle at ray time t is p + t * m (trianglemesh_full.cpp:104-109).
+struct GpuTriMotion {
+  float p1[3], p2[3];
+  float m0[3], m1[3], m2[3];
+  float pad;
+};
+static_assert(sizeof(GpuTriMotion) == 64, "moving tri record size");
 
 struct GpuGeom {
   int32_t kind, material, light, flags;
@@ -88,6 +99,17 @@ struct GpuTexture {
   int64_t offset;  // byte offset of the image in the texel pool
 };
 static_assert(sizeof(GpuTexture) == 32, "texture record is 32 B");
+
+// Everything the shade kernel needs about a hit's geometry in one record: the geometry, a copy
+// of its material and of the material's first texture descriptor (tex[0]: Kd / map_d). The
+// chain hit -> index -> geometry -> material -> texture -> texels becomes hit -> index ->
+// record -> texels: two dependent loads fewer per shaded vertex (k_shade is latency-bound).
+struct GpuGeomRec {
+  GpuGeom g;
+  GpuMaterial m;  // zero when the geometry has no material (g.material < 0)
+  GpuTexture t0;  // m.tex[0]'s descriptor (zero when none)
+};
+static_assert(sizeof(GpuGeomRec) % 16 == 0, "16-byte aligned records");
 
 enum LightType : int32_t {
   LIGHT_AMBIENT = 0,

@@ -495,7 +495,7 @@ struct Collapser {
 }  // namespace
 
 void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const std::vector<uint32_t>& flags,
-               int stackDepth, BvhResult& out) {
+               int stackDepth, BvhResult& out, const std::vector<float>* v1) {
   const int N = (int)(v.size() / 9);
   out.nodes.clear();
   out.tris.clear();
@@ -509,13 +509,13 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
   // spatial splits are opt-in (YRT_SBVH=1): on the measured scenes (C2-C4 stand-ins) they cut
   // node visits by < 1 % for 2-5x the build time
   const char* env = getenv("YRT_SBVH");
-  const bool spatial = env && atoi(env) != 0;
+  const bool spatial = env && atoi(env) != 0 && !v1;  // spatial splits clip static triangles only
   if (N == 1) {
     Node2 n;
-    for (int k = 0; k < 3; ++k) {
-      n.b[0].lo[k] = std::min(std::min(v[k], v[3 + k]), v[6 + k]);
-      n.b[0].hi[k] = std::max(std::max(v[k], v[3 + k]), v[6 + k]);
-    }
+    n.b[0].reset();
+    for (int k = 0; k < 3; ++k) n.b[0].growP(&v[3 * k]);
+    if (v1)
+      for (int k = 0; k < 3; ++k) n.b[0].growP(&(*v1)[3 * k]);
     n.b[1] = n.b[0];
     n.idx[0] = 0; n.cnt[0] = 1;
     n.idx[1] = 0; n.cnt[1] = 1;
@@ -549,6 +549,8 @@ void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const st
       Prim& p = B.prims[i];
       p.b.reset();
       for (int k = 0; k < 3; ++k) p.b.growP(&v[(size_t)i * 9 + 3 * k]);
+      if (v1)
+        for (int k = 0; k < 3; ++k) p.b.growP(&(*v1)[(size_t)i * 9 + 3 * k]);
       for (int k = 0; k < 3; ++k) p.c[k] = 0.5f * (p.b.lo[k] + p.b.hi[k]);
       p.id = i;
     }

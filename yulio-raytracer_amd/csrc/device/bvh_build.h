@@ -17,6 +17,9 @@ struct BvhResult {
 };
 
 // v: 9 floats (v0,v1,v2) per global triangle id; flags: per-triangle GpuTri flags (bit0 cull)
-void build_bvh(const std::vector<float>& v, const std::vector<uint32_t>& flags, int stackDepth, BvhResult& out);
+// v1 (optional): the triangles' vertices at the end of the frame time (moving geometry); the
+// boxes then bound both (trianglemesh_full.cpp:152-166), the leaf records hold the t = 0 triangle
+void build_bvh(const std::vector<float>& v, const std::vector<uint32_t>& flags, int stackDepth, BvhResult& out,
+               const std::vector<float>* v1 = nullptr);
 
 }  // namespace yrt

@@ -51,6 +51,7 @@ struct GpuCtx {
   struct Lane {
     hipStream_t stream = nullptr;
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
+    DevBuf qTime[2], sTime;  // ray times (moving scenes only)
     int64_t pathCap = 0, shadowCap = 0;
     unsigned* hc = nullptr;  // pinned copy of the counters of the lane's last batch
     size_t hcWords = 0;
@@ -99,7 +100,7 @@ struct GpuCtx {
     return dSpill.as<int>();
   }
   // P paths per batch; queues hold YRT_QSEGS segments of qseg_capacity(P) slots
-  static void ensure_paths(Lane& L, int64_t P, int numLights) {
+  static void ensure_paths(Lane& L, int64_t P, int numLights, bool motion) {
     const int64_t Q = (int64_t)YRT_QSEGS * qseg_capacity(P);
     if (Q > L.pathCap) {
       for (int k = 0; k < 2; ++k) {
@@ -120,6 +121,10 @@ struct GpuCtx {
       L.sContrib.alloc(S * 16);
       L.sOcc.alloc(S * 4);
       L.shadowCap = S;
+    }
+    if (motion) {
+      for (int k = 0; k < 2; ++k) L.qTime[k].alloc(Q * 4);
+      L.sTime.alloc(S * 4);
     }
   }
   // ray capture (roofline accounting): strided sample of each depth's query streams, batch 0
@@ -505,7 +510,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
-      GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights);
+      GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights, G.hasMotion);
       L.counters.alloc(counterWords * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
       if (L.hcWords < counterWords) {
@@ -537,6 +542,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.sContrib = L.sContrib.as<float4>();
       pb.sOcc = L.sOcc.as<int>();
       pb.counters = L.counters.as<unsigned>();
+      for (int k = 0; k < 2; ++k) pb.qTime[k] = G.hasMotion ? L.qTime[k].as<float>() : nullptr;
+      pb.sTime = G.hasMotion ? L.sTime.as<float>() : nullptr;
       pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
       pb.segCap = qseg_capacity(pb.capacity);
       pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
@@ -597,7 +604,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         EvPair e1{};
         if (kernelTiming) { e1 = {g.ev(), g.ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
         launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                             pb.segCap, pb.hit, st, hint(estClosest[d]));
+                             pb.segCap, pb.hit, st, hint(estClosest[d]), pb.qTime[cur]);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
           g.capture(captureMax, g.capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0),
@@ -611,7 +618,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           if (kernelTiming) { e3 = {g.ev(), g.ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
           const ShadowFuse sf{pb.sContrib, pb.pathL};
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr, hint(estShadow[d]));
+                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr, hint(estShadow[d]), pb.sTime);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
             g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),

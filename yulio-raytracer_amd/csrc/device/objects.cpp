@@ -225,6 +225,10 @@ std::shared_ptr<const MeshInst> MeshInst::transform(const A3& xfm) const {
   auto t = std::make_shared<MeshInst>(*this);
   for (auto& p : t->pos) p = xfmPoint(xfm, p);
   for (auto& n : t->nor) n = xfmNormal(xfm, n);
+  // motions and tangents are vectors (trianglemesh_full.cpp:79-85)
+  for (auto& m : t->mot) m = xfmVector(xfm, m);
+  for (auto& v : t->tanX) v = xfmVector(xfm, v);
+  for (auto& v : t->tanY) v = xfmVector(xfm, v);
   return t;
 }
 
@@ -240,12 +244,15 @@ void ShapeObj::commit() {
     const Variant* tc = parms.find("texcoords");
     const Variant* tc0 = parms.find("texcoords0");
     const Variant* idx = parms.find("indices");
-    if (mot) throw std::runtime_error("motion blur meshes are not supported by the MI355X device");
-    if (tx || ty) throw std::runtime_error("mesh tangents are not supported by the MI355X device");
-    const bool withNormals = pos && nor && !tc && !tc0;
+    // TriangleMesh::create (shapes/trianglemesh.h:29-41): WithNormals only without motions,
+    // tangents and texcoords
+    const bool withNormals = pos && !mot && nor && !tx && !ty && !tc && !tc0;
     m->kind = withNormals ? GEOM_MESH_NORMALS : GEOM_MESH_FULL;
     if (pos) read_array3(pos, m->pos);
     if (nor) read_array3(nor, m->nor);
+    if (mot) read_array3(mot, m->mot);
+    if (tx) read_array3(tx, m->tanX);
+    if (ty) read_array3(ty, m->tanY);
     const Variant* t = tc0 ? tc0 : tc;
     if (t) {
       auto d = std::dynamic_pointer_cast<DataObj>(t->obj);
@@ -271,6 +278,12 @@ void ShapeObj::commit() {
     if (m->kind == GEOM_MESH_FULL) {
       if (!m->nor.empty() && m->nor.size() < m->pos.size()) throw std::runtime_error("normal count < vertex count");
       if (!m->uv.empty() && m->uv.size() / 2 < m->pos.size()) throw std::runtime_error("texcoord count < vertex count");
+      if (!m->mot.empty() && m->mot.size() < m->pos.size()) throw std::runtime_error("motion count < vertex count");
+      if (!m->tanX.empty() && m->tanX.size() < m->pos.size()) throw std::runtime_error("tangent_x count < vertex count");
+      if (!m->tanY.empty() && m->tanY.size() < m->pos.size()) throw std::runtime_error("tangent_y count < vertex count");
+      m->mot.resize(m->mot.empty() ? 0 : m->pos.size());
+      m->tanX.resize(m->tanX.empty() ? 0 : m->pos.size());
+      m->tanY.resize(m->tanY.empty() ? 0 : m->pos.size());
     }
     for (int v : m->tri)
       if (v < 0 || (size_t)v >= m->pos.size()) throw std::runtime_error("triangle index out of range");
@@ -282,7 +295,7 @@ void ShapeObj::commit() {
     const float r = parms.getFloat("r");
     const size_t numTheta = (size_t)parms.getInt("numTheta");
     const size_t numPhi = (size_t)parms.getInt("numPhi");
-    if (dPdt != v3s(0.f)) throw std::runtime_error("moving spheres are not supported by the MI355X device");
+
     auto eval = [](float theta, float phi) {
       return v3(sinf(theta) * cosf(phi), cosf(theta), sinf(theta) * sinf(phi));
     };
@@ -295,6 +308,7 @@ void ShapeObj::commit() {
         V3 dpdv = eval(float(theta) * kPi * rcpNumTheta, (float(phi) + 0.001f) * 2.0f * kPi * rcpNumPhi) - p;
         p = r * p + P;
         m->pos.push_back(p);
+        if (dPdt != v3s(0.f)) m->mot.push_back(dPdt);  // sphere.h:67
         m->nor.push_back(normalize(cross(dpdv, dpdu)));
         m->uv.push_back(float(phi) * rcpNumPhi);
         m->uv.push_back(float(theta) * rcpNumTheta);

@@ -96,6 +96,8 @@ struct MeshInst {
   std::vector<V3> pos, nor;
   std::vector<float> uv;      // 2 per vertex
   std::vector<int> tri;       // 3 per triangle
+  std::vector<V3> mot;        // per-vertex motion ("motions", Sphere dPdt): empty when static
+  std::vector<V3> tanX, tanY; // per-vertex tangents ("tangent_x" / "tangent_y"): empty when absent
   bool cull = false;
   V3 Ng = v3s(0.f);           // GEOM_TRIANGLE: normalize(cross(v2-v0, v1-v0))
   std::shared_ptr<const MeshInst> transform(const A3& xfm) const;

@@ -27,6 +27,7 @@ static void bind_view(GpuScene& S) {
   v.normals = S.normals.as<float4>();
   v.texcoords = S.texcoords.as<float2>();
   v.geoms = S.geoms.as<GpuGeom>();
+  v.geomRecs = S.geomRecs.as<GpuGeomRec>();
   v.materials = S.materials.as<GpuMaterial>();
   v.textures = S.textures.as<GpuTexture>();
   v.images = S.images.as<GpuImage>();
@@ -35,6 +36,9 @@ static void bind_view(GpuScene& S) {
   v.lights = S.lights.as<GpuLight>();
   v.envLights = S.envLights.as<int>();
   v.media = S.media.as<float4>();
+  v.motions = S.motions.as<float4>();
+  v.tangents = S.tangents.as<float4>();
+  v.triMotion = S.triMotion.as<GpuTriMotion>();
   v.hdriDist = nullptr;
 }
 
@@ -44,8 +48,15 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   auto S = std::make_shared<GpuScene>();
   if (upload) HIP_CHECK(hipGetDevice(&S->device));
 
-  std::vector<float4> positions, normals;
+  std::vector<float4> positions, normals, motions, tangents;  // tangents: (x, y) per vertex
   std::vector<float2> texcoords;
+  bool anyMotion = false, anyTangent = false;
+  for (const auto& p : prims)
+    if (p && p->shape) {
+      anyMotion |= !p->shape->mot.empty();
+      anyTangent |= !p->shape->tanX.empty() || !p->shape->tanY.empty();
+    }
+  std::vector<float> triVerts1;  // moving scenes: the triangles at the end of the frame time
   std::vector<int4> indices;
   std::vector<int> triGeom;
   std::vector<float> triVerts;
@@ -197,7 +208,9 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     g.shadowMask = p->shadowMask;
     g.vtxBase = (int)positions.size();
     g.triBase = gidBase;
-    g.flags = (m.nor.empty() ? 0 : GF_NORMALS) | (m.uv.empty() ? 0 : GF_TEXCOORDS) | (m.cull ? GF_CULL : 0);
+    g.flags = (m.nor.empty() ? 0 : GF_NORMALS) | (m.uv.empty() ? 0 : GF_TEXCOORDS) | (m.cull ? GF_CULL : 0) |
+              (m.mot.empty() ? 0 : GF_MOTION) | (m.tanX.empty() ? 0 : GF_TANGENT_X) |
+              (m.tanY.empty() ? 0 : GF_TANGENT_Y);
     g.Ng[0] = m.Ng.x; g.Ng[1] = m.Ng.y; g.Ng[2] = m.Ng.z;
     const int geomId = (int)geoms.size();
     for (size_t k = 0; k < m.pos.size(); ++k) {
@@ -206,6 +219,15 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
       else normals.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
       if (!m.uv.empty()) texcoords.push_back(make_float2(m.uv[2 * k], m.uv[2 * k + 1]));
       else texcoords.push_back(make_float2(0.f, 0.f));
+      if (anyMotion)
+        motions.push_back(m.mot.empty() ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                        : make_float4(m.mot[k].x, m.mot[k].y, m.mot[k].z, 0.f));
+      if (anyTangent) {
+        tangents.push_back(m.tanX.empty() ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                          : make_float4(m.tanX[k].x, m.tanX[k].y, m.tanX[k].z, 0.f));
+        tangents.push_back(m.tanY.empty() ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                          : make_float4(m.tanY[k].x, m.tanY[k].y, m.tanY[k].z, 0.f));
+      }
     }
     const int nt = (int)(m.tri.size() / 3);
     for (int t = 0; t < nt; ++t) {
@@ -215,6 +237,13 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
       const V3 va = m.pos[a], vb = m.pos[b], vc = m.pos[c];
       const float tv[9] = {va.x, va.y, va.z, vb.x, vb.y, vb.z, vc.x, vc.y, vc.z};
       triVerts.insert(triVerts.end(), tv, tv + 9);
+      if (anyMotion) {  // p + m: the vertices at time 1 (trianglemesh_full.cpp:152-166)
+        const V3 z = v3s(0.f);
+        const V3 ma = m.mot.empty() ? z : m.mot[a], mb = m.mot.empty() ? z : m.mot[b], mc = m.mot.empty() ? z : m.mot[c];
+        const V3 qa = va + ma, qb = vb + mb, qc = vc + mc;
+        const float tv1[9] = {qa.x, qa.y, qa.z, qb.x, qb.y, qb.z, qc.x, qc.y, qc.z};
+        triVerts1.insert(triVerts1.end(), tv1, tv1 + 9);
+      }
       triFlags.push_back(m.cull ? 1u : 0u);
     }
     gidBase += nt;
@@ -223,7 +252,8 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   if (gidBase >= (1 << 26)) throw std::runtime_error("scene exceeds 2^26 triangles (stack entry packing)");
 
   BvhResult bvh;
-  build_bvh(triVerts, triFlags, stackDepth, bvh);
+  build_bvh(triVerts, triFlags, stackDepth, bvh, anyMotion ? &triVerts1 : nullptr);
+  S->hasMotion = anyMotion;
   S->bvhDepth = bvh.maxDepth;
   S->numTris = gidBase;
   S->numGeoms = (int)geoms.size();
@@ -260,9 +290,44 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->triGeom.upload(triGeom);
   S->indices.upload(indices);
   S->positions.upload(positions);
+  if (anyMotion) {
+    S->motions.upload(motions);
+    // per leaf slot: the moving triangle's other vertices and the vertex motions
+    std::vector<GpuTriMotion> tm(bvh.tris.size());
+    for (size_t i = 0; i < bvh.tris.size(); ++i) {
+      const int gid = bvh.order[i];
+      const int4 ix = indices[gid];
+      const int vtx[3] = {ix.x, ix.y, ix.z};
+      GpuTriMotion& r = tm[i];
+      memset(&r, 0, sizeof(r));
+      const float4 p1 = positions[vtx[1]], p2 = positions[vtx[2]];
+      r.p1[0] = p1.x; r.p1[1] = p1.y; r.p1[2] = p1.z;
+      r.p2[0] = p2.x; r.p2[1] = p2.y; r.p2[2] = p2.z;
+      float* ms[3] = {r.m0, r.m1, r.m2};
+      for (int k = 0; k < 3; ++k) {
+        const float4 mv = motions[vtx[k]];
+        ms[k][0] = mv.x; ms[k][1] = mv.y; ms[k][2] = mv.z;
+      }
+    }
+    S->triMotion.upload(tm);
+  }
+  if (anyTangent) S->tangents.upload(tangents);
   S->normals.upload(normals);
   S->texcoords.upload(texcoords);
   S->geoms.upload(geoms);
+  {
+    std::vector<GpuGeomRec> recs(geoms.size());
+    for (size_t i = 0; i < geoms.size(); ++i) {
+      GpuGeomRec& r = recs[i];
+      memset(&r, 0, sizeof(r));
+      r.g = geoms[i];
+      if (r.g.material >= 0) {
+        r.m = materials[r.g.material];
+        if (r.m.tex[0] >= 0) r.t0 = textures[r.m.tex[0]];
+      }
+    }
+    S->geomRecs.upload(recs);
+  }
   S->materials.upload(materials);
   S->textures.upload(textures);
   S->images.upload(images);
@@ -362,6 +427,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   copy(R->normals, src.normals);
   copy(R->texcoords, src.texcoords);
   copy(R->geoms, src.geoms);
+  copy(R->geomRecs, src.geomRecs);
   copy(R->materials, src.materials);
   copy(R->textures, src.textures);
   copy(R->images, src.images);
@@ -370,6 +436,10 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   copy(R->lights, src.lights);
   copy(R->envLights, src.envLights);
   copy(R->media, src.media);
+  copy(R->motions, src.motions);
+  copy(R->triMotion, src.triMotion);
+  copy(R->tangents, src.tangents);
+  R->hasMotion = src.hasMotion;
   R->view = src.view;
   bind_view(*R);
   R->materialMask = src.materialMask;
@@ -383,7 +453,8 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
 }
 
 bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>& prims, hipStream_t stream) {
-  if (!S.nodes.p || prims.size() != S.slotsCommitted.size() || S.hNodes.empty()) return false;
+  // moving geometry: boxes span the frame time and leaf records carry motion (rebuild instead)
+  if (!S.nodes.p || prims.size() != S.slotsCommitted.size() || S.hNodes.empty() || S.hasMotion) return false;
   std::vector<size_t> moved;
   for (size_t i = 0; i < prims.size(); ++i) {
     const auto& o = S.slotsCommitted[i];

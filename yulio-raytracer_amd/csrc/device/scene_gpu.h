@@ -59,7 +59,8 @@ struct GpuScene {
     return n++;
   }
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
-      lights, envLights, hdriDist, media;
+      lights, envLights, hdriDist, media, geomRecs, motions, tangents, triMotion;
+  bool hasMotion = false;  // moving geometry: time-aware trace kernels, no refit
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)
   size_t texels8Bytes = 0;    // the 8-bit images' part of the texel pool (float images follow it)

@@ -263,6 +263,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
     const int p = base + threadIdx.x;
     bool valid = false;
     V3 org = v3s(0.f), dir = v3s(0.f);
+    float rtime = 0.f;
     if (p < P) {  // P and numPixels are multiples of 256: whole waves are in or out
       const int s = p / bi.numPixels, i = p - s * bi.numPixels;
       int x, y, f;
@@ -276,6 +277,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
         const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
         const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
         camera_ray(cam, fx, fy, org, dir, samp(fv, 2, rec), samp(fv, 3, rec));  // sample.getLens()
+        if (pb.qTime[0]) rtime = samp(fv, 4, rec);  // primary.time = sample.getTime() (:159)
       }
       // loop head of Li: depth < maxDepth and max(throughput)=1 >= minContribution
       valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
@@ -288,6 +290,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
       pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
       pb.qThr[0][q] = make_float4(1.f, 1.f, 1.f, __int_as_float((0) | (0 << 8) | (1 << 9)));
+      if (pb.qTime[0]) pb.qTime[0][q] = rtime;
     }
   }
 }
@@ -361,14 +364,35 @@ __device__ __forceinline__ void shadow_done(const ShadowFuse& sf, int* __restric
   }
 }
 
-template <bool ANY>
+// A leaf triangle as tested at ray time t: static scenes read the GpuTri as stored; moving
+// scenes (MOTION) rebuild v0, e1, e2 from p + t * m (trianglemesh_full.cpp:104-109, the same
+// operations as the oracle's trace), keeping the record's id and flag words.
+template <bool MOTION>
+__device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const GpuTriMotion* __restrict__ tms,
+                                         int slot, float time) {
+  GpuTri t = tris[slot];
+  if constexpr (MOTION) {
+    const GpuTriMotion m = tms[slot];
+    const float p0x = t.v0[0] + time * m.m0[0], p0y = t.v0[1] + time * m.m0[1], p0z = t.v0[2] + time * m.m0[2];
+    const float p1x = m.p1[0] + time * m.m1[0], p1y = m.p1[1] + time * m.m1[1], p1z = m.p1[2] + time * m.m1[2];
+    const float p2x = m.p2[0] + time * m.m2[0], p2y = m.p2[1] + time * m.m2[1], p2z = m.p2[2] + time * m.m2[2];
+    t.v0[0] = p0x; t.v0[1] = p0y; t.v0[2] = p0z;
+    t.e1[0] = p0x - p1x; t.e1[1] = p0y - p1y; t.e1[2] = p0z - p1z;
+    t.e2[0] = p2x - p0x; t.e2[1] = p2y - p0y; t.e2[2] = p2z - p0z;
+  }
+  return t;
+}
+
+// MOTION: moving geometry; rayTime[q] is query q's time (Ray::time, set from sample.getTime()
+// for camera rays and inherited by shadow and continuation rays, pathtraceintegrator.cpp:158,210)
+template <bool ANY, bool MOTION>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
-                                                         ShadowFuse sf) {
+                                                         ShadowFuse sf, const float* __restrict__ rayTime) {
   constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
   __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
@@ -426,6 +450,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // ray kept as plain vectors across iterations (a loop-carried RayPre struct ends up in
   // scratch: the vectorizer's straddling loads defeat SROA); rebuilt in registers per step
   float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro, ri = ro, rc = ro;
+  float rtime = 0.f;
   Hit best;
   best.t = best.u = best.v = 0.f;
   best.tri = -1;
@@ -463,6 +488,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             q = qmap_phys(qm, segCap, li);
             ro = org[q];
             rd = dir[q];
+            if (MOTION) rtime = rayTime[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
             {
@@ -604,7 +630,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         if (lTake > 0) {
           GpuTri tt[K];
 #pragma unroll
-          for (int k = 0; k < K; ++k) tt[k] = tris[lIdx + min(k, lTake - 1)];
+          for (int k = 0; k < K; ++k) tt[k] = tri_at<MOTION>(tris, sv.triMotion, lIdx + min(k, lTake - 1), rtime);
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             float t, U, V, absDen;
@@ -621,7 +647,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         }
       } else {
         for (int i = 0; i < lTake && !found; ++i) {
-          const GpuTri tr = tris[lIdx + i];
+          const GpuTri tr = tri_at<MOTION>(tris, sv.triMotion, lIdx + i, rtime);
           float t, U, V, absDen;
           bool ok = tri_test_t(tr, r, ANY ? r.tfar : best.t + 0.0f, t, U, V, absDen);
           const int gid = __float_as_int(tr.v0[3]);
@@ -667,10 +693,11 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 
 // ---------------------------------------------------------------- shading helpers
 // BackendSceneFlat::postIntersect -> Shape::postIntersect
-__device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid, DG& dg,
-                               bool wantTangents) {
-  const int g = sv.indices[gid].w;  // geometry id rides in the index record
-  const GpuGeom geom = sv.geoms[g];
+// geom: the hit triangle's geometry record (sv.geoms / the geometry part of sv.geomRecs)
+// time: the ray's time (moving geometry, GF_MOTION: vertices p + time * m, trianglemesh_full.cpp:211-215)
+__device__ __forceinline__ void post_intersect_g(const SceneView& sv, const GpuGeom& geom, V3 org, V3 dir, float t,
+                                                 float u, float v, int gid, DG& dg, bool wantTangents,
+                                                 float time = 0.f) {
   dg.material = geom.material;
   dg.light = geom.light;
   dg.illumMask = geom.illumMask;
@@ -685,7 +712,12 @@ __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 d
     dg.Tx = dg.Ty = v3s(0.f);
   } else {
     const int4 idx = sv.indices[gid];
-    const V3 p0 = ld3(sv.positions[idx.x]), p1 = ld3(sv.positions[idx.y]), p2 = ld3(sv.positions[idx.z]);
+    V3 p0 = ld3(sv.positions[idx.x]), p1 = ld3(sv.positions[idx.y]), p2 = ld3(sv.positions[idx.z]);
+    if (geom.flags & GF_MOTION) {
+      p0 = p0 + time * ld3(sv.motions[idx.x]);
+      p1 = p1 + time * ld3(sv.motions[idx.y]);
+      p2 = p2 + time * ld3(sv.motions[idx.z]);
+    }
     const float w = 1.0f - u - v;
     const V3 dPdu = p1 - p0, dPdv = p2 - p0;
     dg.Ng = normalize(cross(p0 - p1, p2 - p0));  // ray.Ng (unnormalized Embree Ng)
@@ -727,16 +759,31 @@ __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 d
         dg.Ns = dg.Ng;
       }
       if (wantTangents) {
-        const V3 dPds = normalize(dPdu * dtdv - dPdv * dtdu);
-        dg.Tx = normalize(dPds - dot(dPds, dg.Ns) * dg.Ns);
-        const V3 dPdt = normalize(dPdv * dsdu - dPdu * dsdv);
-        dg.Ty = normalize(dPdt - dot(dPdt, dg.Ns) * dg.Ns);
+        // trianglemesh_full.cpp:244-263: interpolated tangents when the mesh has them
+        if (geom.flags & GF_TANGENT_X) {
+          dg.Tx = w * ld3(sv.tangents[2 * idx.x]) + u * ld3(sv.tangents[2 * idx.y]) + v * ld3(sv.tangents[2 * idx.z]);
+        } else {
+          const V3 dPds = normalize(dPdu * dtdv - dPdv * dtdu);
+          dg.Tx = normalize(dPds - dot(dPds, dg.Ns) * dg.Ns);
+        }
+        if (geom.flags & GF_TANGENT_Y) {
+          dg.Ty = w * ld3(sv.tangents[2 * idx.x + 1]) + u * ld3(sv.tangents[2 * idx.y + 1]) +
+                  v * ld3(sv.tangents[2 * idx.z + 1]);
+        } else {
+          const V3 dPdt = normalize(dPdv * dsdu - dPdu * dsdv);
+          dg.Ty = normalize(dPdt - dot(dPdt, dg.Ns) * dg.Ns);
+        }
       } else {
         dg.Tx = dg.Ty = v3s(0.f);
       }
     }
   }
   dg.error = fmaxf(fabsf(t), reduce_max(absv(dg.P)));
+}
+__device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid,
+                                               DG& dg, bool wantTangents) {
+  const int g = sv.indices[gid].w;  // geometry id rides in the index record
+  post_intersect_g(sv, sv.geoms[g], org, dir, t, u, v, gid, dg, wantTangents);
 }
 
 __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V3 R, float a = 0.f, float b = 0.f,
@@ -758,8 +805,9 @@ __device__ __forceinline__ void add_comp(BRDFSet& bs, int kind, uint32_t type, V
 
 // Material::shade for the in-scope materials (materials/*.h). May modify dg.Ns (Obj bump).
 template <unsigned MM>
-__device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, int matId, int medium, DG& dg,
-                                               BRDFSet& bs) {
+// t0: the descriptor of m.tex[0] (GpuGeomRec::t0)
+__device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMaterial& m, const GpuTexture& t0, int matId,
+                                               int medium, DG& dg, BRDFSet& bs) {
   bs.n = 0;
   // each case is compiled only when the instantiation's material set MM holds its type
   const float idBits = __int_as_float(matId);
@@ -813,7 +861,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       if constexpr (!(MM & mat_bit(MAT_MATTE_TEXTURED))) break;
       if (m.tex[0] >= 0) {
         float c[4];
-        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
+        tex_get_rec(t0, sv.texels, sv.texQuads, m.p[2] * dg.s + m.p[0], m.p[3] * dg.t + m.p[1], c);
         add_comp(bs, C_LAMBERT, BT_DIFFUSE_REFLECTION, v3(c[0], c[1], c[2]));
       }
       break;
@@ -841,7 +889,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       }
       float d = m.p[0];
       if (m.tex[0] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], dg.s, dg.t, c);
+        tex_get_rec(t0, sv.texels, sv.texQuads, dg.s, dg.t, c);
         d *= c[0];
       }
       if (d < 1.0f) add_comp(bs, C_TRANSMISSION, BT_SPECULAR_TRANSMISSION, v3s(1.0f - d));
@@ -871,7 +919,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
       float alpha = 1.f, opacity = 0.f;
       if (m.tex[0] >= 0) {
-        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+        tex_get_rec(t0, sv.texels, sv.texQuads, m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
         alpha = dc[3];
         opacity = 1.f - alpha;
       }
@@ -888,7 +936,7 @@ __device__ __forceinline__ void shade_material(const SceneView& sv, const GpuMat
       add_comp(bs, C_DIEL_REFL, BT_SPECULAR_REFLECTION, v3s(0.f), m.p[10], 1.0f);
       float dc[4] = {m.p[0], m.p[1], m.p[2], 1.f};
       if (m.tex[0] >= 0)
-        tex_get(sv.textures, sv.images, sv.texels, sv.texQuads, m.tex[0], m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
+        tex_get_rec(t0, sv.texels, sv.texQuads, m.p[5] * dg.s + m.p[3], m.p[6] * dg.t + m.p[4], dc);
       const float tr = m.p[9];
       const V3 T = v3(dc[0] * tr, dc[1] * tr, dc[2] * tr);
       add_comp(bs, C_THIN_DIEL_TRANS, BT_SPECULAR_TRANSMISSION, v3(yrt_logf(T.x), yrt_logf(T.y), yrt_logf(T.z)), m.p[10],
@@ -1131,15 +1179,16 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     SPROF_MARK(1);  // misses: environment / backplate
     bool backfacing = false;
+    int g = 0;  // the hit's geometry (sv.geomRecs)
     if (active && isHit) {
       const int gid = __float_as_int(h.w);
-      const int g = sv.indices[gid].w;  // geometry id rides in the index record
-      const int mat = sv.geoms[g].material;
+      g = sv.indices[gid].w;  // geometry id rides in the index record
+      const GpuGeomRec& gr = sv.geomRecs[g];
+      const int mat = gr.g.material;
       // tangents only feed the Obj bump map and the anisotropic microfacet
-      const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && sv.materials[mat].type == MAT_OBJ &&
-                                       sv.materials[mat].tex[4] >= 0) ||
-                                      ((MM & mat_bit(MAT_BRUSHED_METAL)) && sv.materials[mat].type == MAT_BRUSHED_METAL));
-      post_intersect(sv, org, dir, h.x, h.y, h.z, gid, dg, wantT);
+      const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && gr.m.type == MAT_OBJ && gr.m.tex[4] >= 0) ||
+                                      ((MM & mat_bit(MAT_BRUSHED_METAL)) && gr.m.type == MAT_BRUSHED_METAL));
+      post_intersect_g(sv, gr.g, org, dir, h.x, h.y, h.z, gid, dg, wantT, pb.qTime[0] ? samp(fv, 4, rec) : 0.f);
       if (dot(dg.Ng, dir) > 0.f) {
         backfacing = true;
         dg.Ng = -dg.Ng;
@@ -1148,7 +1197,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
     SPROF_MARK(2);  // postIntersect
     if (active && isHit) {
-      if (dg.material >= 0) shade_material<MM>(sv, sv.materials[dg.material], dg.material, medium, dg, bs);
+      if (dg.material >= 0) shade_material<MM>(sv, sv.geomRecs[g].m, sv.geomRecs[g].t0, dg.material, medium, dg, bs);
       if (!ignoreVL && dg.light >= 0 && !backfacing) {
         const GpuLight& al = sv.lights[dg.light];
         if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
@@ -1219,6 +1268,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
     if (haveL) pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);
     if (got) {
+      if (pb.qTime[0]) pb.qTime[cur ^ 1][nq] = samp(fv, 4, rec);  // lastRay.time (:210)
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
       pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
@@ -1271,6 +1321,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       bool sgot;
       const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
       if (sgot) {
+        if (pb.sTime) pb.sTime[si] = samp(fv, 4, rec);  // lastRay.time (:158)
         pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
         pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
         pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
@@ -1466,18 +1517,29 @@ static inline long long hinted(long long maxCount, long long hint) {
 }
 
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint) {
+                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint, const float* time) {
   const long long maxCount = hinted((long long)numSegs * segCap, countHint);
-  hipLaunchKernelGGL(k_trace<false>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{});
+  const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+  if (time)
+    hipLaunchKernelGGL((k_trace<false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
+                       hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, time);
+  else
+    hipLaunchKernelGGL((k_trace<false, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                       segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr);
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, long long countHint) {
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, long long countHint,
+                      const float* time) {
   const long long maxCount = hinted((long long)numSegs * segCap, countHint);
-  hipLaunchKernelGGL(k_trace<true>, dim3(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID)), dim3(YRT_TRACE_BLOCK),
-                     0, s, sv, org, dir, counts, numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill,
-                     fuse ? *fuse : ShadowFuse{});
+  const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+  if (time)
+    hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
+                       (float4*)nullptr, occluded, sv.traceSpill, fuse ? *fuse : ShadowFuse{}, time);
+  else
+    hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                       segCap, (float4*)nullptr, occluded, sv.traceSpill, fuse ? *fuse : ShadowFuse{},
+                       (const float*)nullptr);
 }
 
 // Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of

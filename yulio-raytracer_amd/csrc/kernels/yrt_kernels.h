@@ -19,6 +19,7 @@ struct SceneView {
   const float4* normals;
   const float2* texcoords;
   const GpuGeom* geoms;
+  const GpuGeomRec* geomRecs;  // per geometry: geometry + material + tex[0] descriptor (k_shade)
   const GpuMaterial* materials;
   const GpuTexture* textures;
   const GpuImage* images;
@@ -28,6 +29,9 @@ struct SceneView {
   const int* envLights;
   const float* hdriDist;
   const float4* media;  // medium table (transmission.rgb, eta); [0] = vacuum (materials/medium.h)
+  const float4* motions;            // per vertex (moving scenes only, else null)
+  const float4* tangents;           // per vertex: tangent_x, tangent_y (meshes with tangents, else null)
+  const GpuTriMotion* triMotion;    // per leaf slot (moving scenes only, else null)
   int* traceSpill;   // deep traversal-stack entries: YRT_TRACE_SPILL_INTS ints
   int numLights, numEnvLights, numNodes, numTris;
 };
@@ -85,6 +89,8 @@ struct PathBuffers {
   float4* sDir;
   float4* sContrib;
   int* sOcc;
+  float* qTime[2];   // moving scenes: ray time per closest-queue slot (else null)
+  float* sTime;      // moving scenes: ray time per shadow slot (else null)
   unsigned* counters;  // segment counters, see qcounter_index
   int capacity;        // max paths
   int segCap;          // closest-queue slots per segment (qPath/qOrg/qDir/hit: YRT_QSEGS * segCap)
@@ -116,11 +122,13 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 // of segCap slots; hit/occluded are indexed by physical slot.
 // countHint (>= 0): expected queue length, sizes the grid (the kernels grid-stride over the
 // real device-side count, so a low hint costs speed, never correctness); -1: full grid.
+// time (moving scenes): per-slot ray time (Ray::time); null: static scene (or time 0)
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1);
+                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1,
+                          const float* time = nullptr);
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr,
-                      long long countHint = -1);
+                      long long countHint = -1, const float* time = nullptr);
 // materialMask: bit MAT_x set for every material type the scene uses (selects a specialized
 // instantiation of the shade kernel)
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,

@@ -196,17 +196,14 @@ __device__ __forceinline__ void texel_u8(uint32_t w, bool rgb, float c[4]) {
   c[2] = ((w >> 16) & 0xffu) * one_over_255;
   c[3] = rgb ? 1.0f : (w >> 24) * one_over_255;
 }
-__device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures, const GpuImage* __restrict__ images,
-                                        const uint8_t* __restrict__ pool, const uint8_t* __restrict__ quads, int texId,
-                                        float px, float py, float out[4]) {
-  const GpuTexture tx = textures[texId];
+__device__ __forceinline__ void tex_get_rec(const GpuTexture& tx, const uint8_t* __restrict__ pool,
+                                            const uint8_t* __restrict__ quads, float px, float py, float out[4]) {
   // the texture record carries its image's descriptor: one dependent load fewer (-2 % shade)
   GpuImage im;
   im.width = tx.width;
   im.height = tx.height;
   im.format = tx.format;
   im.offset = tx.offset;
-  (void)images;
   const float s1 = px - floorf(px), t1 = py - floorf(py);
   float c[4];
   if (tx.filter == TEX_BILINEAR) {
@@ -250,6 +247,13 @@ __device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures,
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) out[k] = c[k];
+}
+__device__ __forceinline__ void tex_get(const GpuTexture* __restrict__ textures, const GpuImage* __restrict__ images,
+                                        const uint8_t* __restrict__ pool, const uint8_t* __restrict__ quads, int texId,
+                                        float px, float py, float out[4]) {
+  (void)images;
+  const GpuTexture tx = textures[texId];
+  tex_get_rec(tx, pool, quads, px, py, out);
 }
 
 // ---------------------------------------------------------------- BRDF components
