@@ -42,6 +42,7 @@ def _sig(name, res, *args):
 _sig("oracle_render", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, vp, C.POINTER(OracleStats))
 _sig("oracle_trace", i32, vp, sz, vp, vp, i32, i32, vp)
 _sig("oracle_debug_pixel", i32, vp, sz, i32, i32, i32, i32, vp, i32)
+_sig("oracle_debug_path", i32, vp, sz, i32, i32, i32, i32, i32, vp)
 _sig("oracle_render_shard", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, i32, i32, vp,
      C.POINTER(OracleStats))
 _sig("oracle_count_visits", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
@@ -94,6 +95,19 @@ def debug_pixel(blob: bytes, width, height, x, y, max_spp=1 << 16):
     if n < 0:
         raise RuntimeError(f"oracle_debug_pixel: {_err()}")
     return out[:min(n, max_spp)]
+
+
+# fields of a debug_path record (32 floats per depth)
+PATH_FIELDS = ["valid", "tri", "t", "u", "v", "thr", "thr", "thr", "P", "P", "P", "Ns", "Ns", "Ns", "L", "L", "L",
+               "wi", "wi", "wi", "pdf", "c", "c", "c", "nthr", "nthr", "nthr", "dir", "dir", "dir", "org_x", "useDirect"]
+
+
+def debug_path(blob: bytes, width, height, x, y, sample):
+    """Per-depth record of sample `sample` of pixel (x, y): float32 (depths, 32), PATH_FIELDS."""
+    out = np.zeros((32, 32), np.float32)
+    if _lib.oracle_debug_path(blob, len(blob), width, height, x, y, sample, out.ctypes.data) < 0:
+        raise RuntimeError(f"oracle_debug_path: {_err()}")
+    return out[: int((out[:, 0] != 0).sum())]
 
 
 def trace(blob: bytes, org4: np.ndarray, dir4: np.ndarray, any_hit=False):

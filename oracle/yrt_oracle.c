@@ -928,7 +928,7 @@ static inline int box_hit(const float* lo, const float* hi, const Ray* r, V3 inv
   }
   const float n = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r->tnear));
   const float f = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), tmax));
-  return n <= f * 1.00000036f;
+  return n <= f * 1.0000152587890625f; /* 1 + 2^-16, as the device (yrt_traverse.h YRT_BOX_ROBUST) */
 }
 static inline float safe_inv(float d) { return 1.0f / (fabsf(d) > 1e-20f ? d : copysignf(1e-20f, d)); }
 
@@ -2036,6 +2036,20 @@ typedef struct {
 } RCfg;
 
 /* PathTraceIntegrator::Li (integrators/pathtraceintegrator.cpp:50-217) */
+/* path debugging (oracle_debug_path): 32 floats per depth of one (pixel, sample), the layout of the
+ * device's YRT_PATH_DEBUG capture in k_shade */
+static float* g_pathDbg = NULL;
+static void path_dbg(int depth, int tri, const Hit* h, V3 thr, const DG* dg, V3 Lem, V3 wi, float pdf, V3 c, V3 nthr,
+                     const Ray* ray, int useDirect) {
+  if (!g_pathDbg || depth >= 32) return;
+  const V3 z = vs(0.f);
+  const V3 P = dg ? dg->P : z, Ns = dg ? dg->Ns : z;
+  const float r[32] = {1.f, (float)tri, h->t, h->u, h->v, thr.x, thr.y, thr.z, P.x, P.y, P.z, Ns.x, Ns.y, Ns.z,
+                       Lem.x, Lem.y, Lem.z, wi.x, wi.y, wi.z, pdf, c.x, c.y, c.z, nthr.x, nthr.y, nthr.z,
+                       ray->dir.x, ray->dir.y, ray->dir.z, ray->org.x, (float)useDirect};
+  memcpy(g_pathDbg + depth * 32, r, sizeof(r));
+}
+
 static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, uint32_t pixelId, int s, uint32_t seed,
              float pixelX, float pixelY /* state.pixel (integratorrenderer.cpp:162) */, double* nClosest,
              double* nShadow) {
@@ -2069,6 +2083,7 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
           else Le = hdri_Le(W, E, wo);
           L = add(L, mulv(thr, Le));
         }
+      if (g_pathDbg) { Hit hz = {0.f, 0.f, 0.f, -1}; path_dbg(depth, -1, &hz, thr, NULL, L, vs(0.f), 0.f, vs(0.f), vs(0.f), &ray, 0); }
       break;
     }
     DG dg;
@@ -2081,6 +2096,9 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
     if (!ignoreVL && dg.light >= 0 && !backfacing) L = add(L, mulv(thr, W->lights[dg.light].L));
     int useDirect = 0;
     for (int i = 0; i < bs.n; i++) useDirect |= (bs.c[i].type & BT_DIFFUSE) != 0;
+    const V3 Lem = L;
+#define PATH_DBG(wi_, pdf_, c_, nthr_) \
+  if (g_pathDbg) path_dbg(depth, h.tri, &h, thr, &dg, Lem, wi_, pdf_, c_, nthr_, &ray, useDirect)
     if (useDirect) {
       for (int li = 0; li < W->nlights; li++) {
         const Light* Lt = &W->lights[li];
@@ -2147,16 +2165,17 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
         L = add(L, muls(mulv(mulv(thr, Ls), brdf), rcp(pdf)));
       }
     }
-    if (depth >= R->maxDepth - 1) break;
+    if (depth >= R->maxDepth - 1) { PATH_DBG(vs(0.f), 0.f, vs(0.f), vs(0.f)); break; }
     if (R->rrDepth > 0 && depth >= R->rrDepth - 1) {
       const float q = fminf(fmax3(thr) * eta * eta, .95f);
-      if (S1(depth) >= q) break;
+      if (S1(depth) >= q) { PATH_DBG(vs(0.f), 0.f, vs(0.f), vs(0.f)); break; }
     }
     V3 wi;
     float pdf;
     uint32_t type;
     V3 c = bs_sample(&bs, wo, &dg, S2X(1 + depth), S2Y(1 + depth), S1(depth), &wi, &pdf, &type);
-    if (v3zero(c) || pdf <= 0.f) break;
+    if (v3zero(c) || pdf <= 0.f) { PATH_DBG(wi, pdf, c, vs(0.f)); break; }
+    const V3 cDbg = c;
     /* simple volumetric effect and medium tracking (pathtraceintegrator.cpp:197-207) */
     if (!veq(medium.T, vs(1.0f)))
       c = mulv(c, v3(yrt_powf(medium.T.x, h.t), yrt_powf(medium.T.y, h.t), yrt_powf(medium.T.z, h.t)));
@@ -2164,6 +2183,8 @@ static V3 Li(const World* W, const RCfg* R, const Table* T, int rec, Ray ray, ui
       const Material* mt = &W->mats[dg.material];
       if (mt->type == MT_DIELECTRIC) medium = med_eq(medium, mt->inside) ? mt->outside : mt->inside;
     }
+    PATH_DBG(wi, pdf, cDbg, muls(mulv(thr, c), rcp(pdf)));
+#undef PATH_DBG
     thr = muls(mulv(thr, c), rcp(pdf));
     ignoreVL = (type & BT_DIFFUSE) != 0;
     unbent = unbent && veq(wi, ray.dir); /* LightPath::extended (pathtraceintegrator.h:45) */
@@ -2393,7 +2414,22 @@ int oracle_render_shard(const void* blob, size_t bytes, int width, int height, f
 
 /* Debug: the per-sample radiance Li of one pixel (the terms the pixel's sum adds in s order),
  * out3[3*s..3*s+2] for s < spp; returns spp (or -1). */
+static int debug_pixel_impl(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3,
+                            int maxSpp, int only);
 int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3, int maxSpp) {
+  return debug_pixel_impl(blob, bytes, width, height, x, y, out3, maxSpp, -1);
+}
+int oracle_debug_path(const void* blob, size_t bytes, int width, int height, int x, int y, int sample, float* out) {
+  float L[3 * 4096];
+  if (sample < 0 || sample >= 4096) return -1;
+  memset(out, 0, sizeof(float) * 32 * 32);
+  g_pathDbg = out;
+  const int r = debug_pixel_impl(blob, bytes, width, height, x, y, L, sample + 1, sample);
+  g_pathDbg = NULL;
+  return r;
+}
+static int debug_pixel_impl(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3,
+                            int maxSpp, int only) {
   Blob B;
   if (blob_parse(blob, bytes, &B)) return -1;
   World W;
@@ -2410,6 +2446,7 @@ int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, in
   double nc = 0, ns = 0;
   const int spp = T.spp;
   for (int s = 0; s < spp && s < maxSpp; s++) {
+    if (only >= 0 && s != only) continue;
     const int rec = set * spp + s;
     const float fx = ((float)x + T.t[rec]) * rcpW;
     const float fy = ((float)y + T.t[(size_t)T.rec + rec]) * rcpH;
@@ -2504,7 +2541,7 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
             for (int a = 0; a < 3; ++a) { l[a] = fmaf(lo[a], iv[a], -oi[a]); h[a] = fmaf(hi[a], iv[a], -oi[a]); }
             const float nn = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
             const float ff = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
-            const int hit = nn <= fmaf(ff, 1.00000036f, margin) && nd->child[k] != -1;
+            const int hit = nn <= fmaf(ff, 1.0000152587890625f, margin) && nd->child[k] != -1;
             t[k] = hit ? nn : INF;
             c[k] = nd->child[k];
           }

@@ -70,6 +70,9 @@ int oracle_render_shard(const void* blob, size_t bytes, int width, int height, f
  * (tri as int bits, -1 miss). anyHit != 0 -> occluded test, hit4.w = 1/0. */
 /* Debug: per-sample radiance Li of pixel (x, y), out3[3*s..] for s < min(spp, maxSpp); returns spp. */
 int oracle_debug_pixel(const void* blob, size_t bytes, int width, int height, int x, int y, float* out3, int maxSpp);
+/* the per-depth record of one sample of one pixel (32 floats per depth, 32 depths), the layout
+ * of the device's YRT_PATH_DEBUG capture: for parity debugging only */
+int oracle_debug_path(const void* blob, size_t bytes, int width, int height, int x, int y, int sample, float* out);
 int oracle_trace(const void* blob, size_t bytes, const float* org4, const float* dir4, int n, int anyHit,
                  float* hit4);
 

@@ -37,5 +37,8 @@ def test_sample_scene_parity(gpu_device, name, face):
     s = yrt.Session(SCENES_ARGS[name] + ["-size", "64", "64", "-spp", "4", "-fb", "RGB_FLOAT32"], device=gpu_device)
     img = s.render(face)
     ref, _ = oracle.render(s.export_frame(face), 64, 64, s.info()["gamma"])
-    parity(img, ref, 0.999)
+    # test_transmissive's ThinDielectric spheres (eta 1, transmission with zero channels): the
+    # restated reference arithmetic gives NaN samples on some paths (log(0) absorption), the
+    # GPU must give them on the same pixels
+    parity(img, ref, 0.999, nan_ok=name == "test_transmissive")
     s.close()

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--size", type=int, default=1536)
     ap.add_argument("--views", type=int, default=1, help="FPR views timed render-only (a)")
     ap.add_argument("--no-startrt", action="store_true")
+    ap.add_argument("--no-cube", action="store_true", help="skip (a') the render-only cube-job timing")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-face", action="store_true", help="skip (a) the face-by-face timing")
     ap.add_argument("--cpu-rows", type=int, default=96)
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "c5_bench.json"))
     a = ap.parse_args()
@@ -55,7 +58,7 @@ def main():
     s = yrt.Session(args(a.spp), device=dev)
     s.render_scene_camera(0)  # untimed: allocations, sample table
     faces, rays, t_faces = [], 0.0, 0.0
-    for v in range(a.views):
+    for v in range(0 if a.no_face else a.views):
         for f in range(12):
             t0 = time.perf_counter()
             img = s.render_scene_camera(12 * v + f)
@@ -68,8 +71,23 @@ def main():
             print(f"face {12 * v + f}: {dt * 1e3:.0f} ms", flush=True)
     samples = 12.0 * a.views * a.size * a.size * a.spp
     res["render"] = {"devices": dev.device_count(), "views": a.views, "seconds": round(t_faces, 3),
-                     "ms_per_cubemap": round(t_faces / a.views * 1e3, 1), "Mrays_per_s": round(rays / t_faces / 1e6, 2),
-                     "Msamples_per_s": round(samples / t_faces / 1e6, 2), "rays": rays, "faces": faces}
+                     "ms_per_cubemap": round(t_faces / a.views * 1e3, 1),
+                     "Mrays_per_s": round(rays / t_faces / 1e6, 2) if t_faces else None,
+                     "Msamples_per_s": round(samples / t_faces / 1e6, 2) if t_faces else None, "rays": rays,
+                     "faces": faces}
+    # (a') render only, each view's 12 faces as one job (yrtRenderFrames: what StartRT runs)
+    if not a.no_cube:
+        t_cube, crays = 0.0, 0.0
+        for v in range(a.views):
+            t0 = time.perf_counter()
+            s.render_scene_cube(v, read=False)
+            t_cube += time.perf_counter() - t0
+            st = dev.render_stats()
+            crays += st["raysClosest"] + st["raysShadow"]
+            print(f"view {v} cube job: {(time.perf_counter() - t0) * 1e3:.0f} ms", flush=True)
+        res["render_cube_job"] = {"seconds": round(t_cube, 3), "ms_per_cubemap": round(t_cube / a.views * 1e3, 1),
+                                  "Mrays_per_s": round(crays / t_cube / 1e6, 2),
+                                  "Msamples_per_s": round(samples / t_cube / 1e6, 2), "rays": crays}
     s.close()
     dev.close()
 
@@ -87,6 +105,11 @@ def main():
         print(f"StartRT: {dt:.1f} s, error {err}, {outs}", flush=True)
 
     # (c) CPU baseline on a band of face 0 at 16 spp, scaled
+    if a.no_cpu:
+        Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.out).write_text(json.dumps(res) + "\n")
+        print(json.dumps({k: v for k, v in res.items() if k != "render"}), flush=True)
+        return
     import oracle
     cpu_spp = 16
     hd = yrt.Device(host=True)

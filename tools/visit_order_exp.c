@@ -159,7 +159,7 @@ int visit_counts(const void* nodes_, size_t nn, const void* tris_, const float* 
           for (int a = 0; a < 3; ++a) { l[a] = fmaf(lo[a], iv[a], -oi[a]); h[a] = fmaf(hi[a], iv[a], -oi[a]); }
           const float a0 = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), tnear));
           const float b0 = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best));
-          const int hit = a0 <= fmaf(b0, 1.00000036f, margin) && nd->child[k] != -1;
+          const int hit = a0 <= fmaf(b0, 1.0000152587890625f, margin) && nd->child[k] != -1;
           t[k] = hit ? a0 : INFINITY;
           c[k] = nd->child[k];
         }
@@ -367,7 +367,7 @@ int visit_counts8(const void* nodes_, size_t nn, const void* tris_, const float*
           for (int a = 0; a < 3; ++a) { l[a] = fmaf(nd->lo[k][a], iv[a], -oi[a]); h[a] = fmaf(nd->hi[k][a], iv[a], -oi[a]); }
           const float a0 = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), tnear));
           const float b0 = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best));
-          const int hit = nd->child[k] != -1 && a0 <= fmaf(b0, 1.00000036f, margin);
+          const int hit = nd->child[k] != -1 && a0 <= fmaf(b0, 1.0000152587890625f, margin);
           t[k] = hit ? a0 : INFINITY;
           c[k] = nd->child[k];
         }

@@ -50,6 +50,22 @@ struct GpuTriMotion {
 };
 static_assert(sizeof(GpuTriMotion) == 64, "moving tri record size");
 
+// Per triangle (global id order): what k_shade's postIntersect reads of a static mesh triangle,
+// in one 96-byte record instead of an index record plus nine vertex gathers (positions,
+// normals, texcoords): e1 = p0 - p1, e2 = p2 - p0 (the geometric normal's edges; p1 - p0 is
+// -e1 bit for bit), the vertex normals and texture coordinates (zero where the mesh has
+// none), and the geometry id. Moving meshes and meshes with tangent arrays keep the indexed path.
+struct GpuTriShade {
+  float e1[3];
+  int32_t geom;
+  float e2[3];
+  float pad0;
+  float n[9];   // n0, n1, n2
+  float st[6];  // st0, st1, st2
+  float pad1;
+};
+static_assert(sizeof(GpuTriShade) == 96, "shade tri record size");
+
 struct GpuGeom {
   int32_t kind, material, light, flags;
   int32_t vtxBase, triBase, illumMask, shadowMask;

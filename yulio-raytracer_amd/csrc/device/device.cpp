@@ -36,6 +36,7 @@ struct FrameCache {
   std::string key;
   SampleTable table;
   DevBuf dims, light;
+  std::vector<uint8_t> slotLive;  // per light-sample slot: some record's radiance is not exactly 0
 };
 
 // One HIP device's rendering state: its streams (lanes), the frame buffers, the wavefront
@@ -61,7 +62,8 @@ struct GpuCtx {
   static constexpr int kMaxLanes = 2;
   Lane lanes[kMaxLanes];
   int numLanes = kMaxLanes;
-  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab;
+  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab, dDirect;
+  std::vector<int> hDirect;        // the frame's direct-light list (uploaded to dDirect)
   std::vector<GpuCamera> hCams;  // the job's cameras, one per frame (uploaded to dCam)
   DevBuf dBackplate;                       // the renderer's backplate image (texels)
   uint64_t backplateSerial = 0;            // ImageObj::serial of the image dBackplate holds
@@ -432,6 +434,13 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     }
     auto fc = std::make_unique<FrameCache>();
     build_sample_table(req, fc->table);
+    const SampleTable& t = fc->table;
+    fc->slotLive.assign(t.numLightSlots, 0);
+    for (int r = 0; r < t.numRecords; ++r)
+      for (int k = 0; k < t.numLightSlots; ++k) {
+        const float* ls = &t.light[((size_t)r * t.numLightSlots + k) * 8];
+        if (!(ls[4] == 0.f && ls[5] == 0.f && ls[6] == 0.f)) fc->slotLive[k] = 1;
+      }
     fc->dims.upload(fc->table.dims);
     fc->light.upload(fc->table.light);
     fc->key = keybuf;
@@ -442,6 +451,25 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   const SampleTable& tab = fcache.table;
   rp.spp = tab.spp;
   rp.sets = tab.sets;
+  // direct lighting (pathtraceintegrator.cpp:123-167) skips a light whose sample radiance is
+  // exactly 0 for every sample of the frame (a zero L, e.g. C4's HDRILight L = 0 0 0): its
+  // shadow ray is never cast, so dropping it from the loop changes no pixel, and a frame left
+  // with one such light fuses the shadow resolve into the any-hit kernel. The loop keeps the
+  // lights' own indices (shadow jitter hash, light order).
+  g.hDirect.clear();
+  for (int li = 0; li < (int)G.hLights.size(); ++li) {
+    const GpuLight& lt = G.hLights[li];
+    const bool live = lt.precomputed >= 0 ? (lt.precomputed < (int)fcache.slotLive.size() && fcache.slotLive[lt.precomputed])
+                                          : !(lt.L[0] == 0.f && lt.L[1] == 0.f && lt.L[2] == 0.f);
+    if (live || getenv("YRT_ALL_DIRECT_LIGHTS")) g.hDirect.push_back(li);
+  }
+  g.dDirect.alloc(sizeof(int) * std::max<size_t>(1, g.hDirect.size()));
+  if (!g.hDirect.empty())
+    HIP_CHECK(hipMemcpyAsync(g.dDirect.p, g.hDirect.data(), sizeof(int) * g.hDirect.size(), hipMemcpyHostToDevice,
+                             stream));
+  sv.directLights = g.dDirect.as<int>();
+  sv.numDirectLights = (int)g.hDirect.size();
+  const int numDirect = sv.numDirectLights;
 
   g.dRp.alloc(sizeof(rp));
   g.hCams.resize(nf);
@@ -510,7 +538,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
-      GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), rp.numLights, G.hasMotion);
+      GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), numDirect, G.hasMotion);
       L.counters.alloc(counterWords * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
       if (L.hcWords < counterWords) {
@@ -546,9 +574,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.sTime = G.hasMotion ? L.sTime.as<float>() : nullptr;
       pb.capacity = (int)std::max<int64_t>(P, 256ll * spp);
       pb.segCap = qseg_capacity(pb.capacity);
-      pb.shSegCap = pb.segCap * std::max(1, rp.numLights);
+      pb.shSegCap = pb.segCap * std::max(1, numDirect);
       // one light: shadow contributions are added by k_trace<true> itself (no resolve pass)
-      pb.fuseShadow = rp.numLights == 1 && !getenv("YRT_NO_SHADOW_FUSE");
+      pb.fuseShadow = numDirect == 1 && !getenv("YRT_NO_SHADOW_FUSE");
       return pb;
     };
     // queue lengths of the last drained batch per depth: grid-size hints for the next batches
@@ -613,7 +641,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
         launch_shade(lsv, fv, pb, bi, d, G.materialMask, st, hint(estClosest[d]));
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
-        if (rp.numLights > 0) {
+        if (numDirect > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {g.ev(), g.ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
           const ShadowFuse sf{pb.sContrib, pb.pathL};
@@ -623,7 +651,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           if (captureMax > 0 && first == 0)
             g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),
                       pb.shSegCap, st);
-          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, rp.numLights, st, hint(estClosest[d]));
+          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st, hint(estClosest[d]));
         }
       }
       launch_resolve_pixels(fv, pb, bi, g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), (int)rgb8Stride,

@@ -28,6 +28,7 @@ static void bind_view(GpuScene& S) {
   v.texcoords = S.texcoords.as<float2>();
   v.geoms = S.geoms.as<GpuGeom>();
   v.geomRecs = S.geomRecs.as<GpuGeomRec>();
+  v.triShade = S.triShade.as<GpuTriShade>();
   v.materials = S.materials.as<GpuMaterial>();
   v.textures = S.textures.as<GpuTexture>();
   v.images = S.images.as<GpuImage>();
@@ -70,6 +71,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   std::vector<uint8_t> texels, texelsF;
   std::vector<GpuLight> lights;
   std::vector<int> envLights;
+  int numEnvZero = 0;
   std::map<const MaterialInst*, int> matIds;
   std::map<const TextureInst*, int> texIds;
   std::map<const ImageObj*, int> imgIds;
@@ -158,7 +160,16 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     // EnvironmentLight subclasses (api/scene.h:76): ambient, HDRI, distant
     if (L.type == LIGHT_AMBIENT || L.type == LIGHT_HDRI || L.type == LIGHT_DISTANT) {
       g.isEnv = 1;
-      envLights.push_back((int)lights.size());
+      // an environment light whose Le is exactly 0 for every direction (L = 0 0 0 over finite
+      // texels, e.g. C4's HDRILight) only adds throughput * 0 to a missed path: k_shade leaves
+      // it out and keeps the NaN such an add makes of a non-finite throughput (numEnvZero)
+      bool zero = L.L.x == 0.f && L.L.y == 0.f && L.L.z == 0.f;
+      if (zero && L.type == LIGHT_HDRI && L.image && L.image->format == IMG_RGBAF32) {
+        const float* f = (const float*)L.image->data.data();
+        for (size_t k = 0; k < L.image->data.size() / 4 && zero; ++k) zero = std::isfinite(f[k]);
+      }
+      if (zero) ++numEnvZero;
+      else envLights.push_back((int)lights.size());
     }
     if (L.type == LIGHT_HDRI) {
       g.image = imageId(L.image);
@@ -316,6 +327,26 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->texcoords.upload(texcoords);
   S->geoms.upload(geoms);
   {
+    std::vector<GpuTriShade> ts(indices.size());
+    for (size_t t = 0; t < indices.size(); ++t) {
+      const int4 ix = indices[t];
+      const int v[3] = {ix.x, ix.y, ix.z};
+      GpuTriShade& r = ts[t];
+      memset(&r, 0, sizeof(r));
+      const float4 p0 = positions[ix.x], p1 = positions[ix.y], p2 = positions[ix.z];
+      r.e1[0] = p0.x - p1.x; r.e1[1] = p0.y - p1.y; r.e1[2] = p0.z - p1.z;
+      r.e2[0] = p2.x - p0.x; r.e2[1] = p2.y - p0.y; r.e2[2] = p2.z - p0.z;
+      r.geom = ix.w;
+      for (int k = 0; k < 3; ++k) {
+        const float4 n = normals[v[k]];
+        r.n[3 * k] = n.x; r.n[3 * k + 1] = n.y; r.n[3 * k + 2] = n.z;
+        r.st[2 * k] = texcoords[v[k]].x;
+        r.st[2 * k + 1] = texcoords[v[k]].y;
+      }
+    }
+    S->triShade.upload(ts);
+  }
+  {
     std::vector<GpuGeomRec> recs(geoms.size());
     for (size_t i = 0; i < geoms.size(); ++i) {
       GpuGeomRec& r = recs[i];
@@ -356,11 +387,13 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
     S->texQuads.upload(quads);
   }
   S->lights.upload(lights);
+  S->hLights = lights;
   S->envLights.upload(envLights);
   S->media.upload(media);
 
   S->view.numLights = (int)lights.size();
   S->view.numEnvLights = (int)envLights.size();
+  S->view.numEnvZero = numEnvZero;
   S->view.numNodes = (int)bvh.nodes.size();
   S->view.numTris = gidBase;
   bind_view(*S);
@@ -428,6 +461,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   copy(R->texcoords, src.texcoords);
   copy(R->geoms, src.geoms);
   copy(R->geomRecs, src.geomRecs);
+  copy(R->triShade, src.triShade);
   copy(R->materials, src.materials);
   copy(R->textures, src.textures);
   copy(R->images, src.images);
@@ -444,6 +478,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   bind_view(*R);
   R->materialMask = src.materialMask;
   R->precomputed = src.precomputed;
+  R->hLights = src.hLights;
   R->numTris = src.numTris;
   R->numGeoms = src.numGeoms;
   R->bvhDepth = src.bvhDepth;
@@ -485,8 +520,9 @@ bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>&
                              hipMemcpyHostToDevice, stream));
     HIP_CHECK(hipMemcpyAsync(S.normals.as<float4>() + g.vtxBase, nor.data(), nor.size() * sizeof(float4),
                              hipMemcpyHostToDevice, stream));
-    launch_refit_tris(S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(), S.triLeaf.as<int>(),
-                      S.triLeaf.as<int>() + S.numTris + 1, g.triBase, (int)(m.tri.size() / 3), stream);
+    launch_refit_tris(S.tris.as<GpuTri>(), S.triShade.as<GpuTriShade>(), S.indices.as<int4>(), S.positions.as<float4>(),
+                      S.normals.as<float4>(), S.triLeaf.as<int>(), S.triLeaf.as<int>() + S.numTris + 1, g.triBase,
+                      (int)(m.tri.size() / 3), stream);
     // the host copies must outlive the async copies
     HIP_CHECK(hipStreamSynchronize(stream));
   }

@@ -59,7 +59,7 @@ struct GpuScene {
     return n++;
   }
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
-      lights, envLights, hdriDist, media, geomRecs, motions, tangents, triMotion;
+      lights, envLights, hdriDist, media, geomRecs, motions, tangents, triMotion, triShade;
   bool hasMotion = false;  // moving geometry: time-aware trace kernels, no refit
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)
@@ -70,6 +70,7 @@ struct GpuScene {
   std::vector<GpuGeom> hGeoms;
   std::vector<int> hTriGeom;
   std::vector<std::shared_ptr<const LightInst>> allLights;
+  std::vector<GpuLight> hLights;                // the uploaded light table
   std::vector<LightSampleSource> precomputed;   // LightSampleSource per precompute() light
   // incremental commits (faceCamera refit, refit_gpu_scene): the slots this scene was built
   // from, slot -> geometry, gid -> leaf position, and the node indices grouped by tree depth

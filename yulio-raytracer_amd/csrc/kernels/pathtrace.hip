@@ -270,7 +270,6 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
       valid = batch_pixel(rp, bi, i, x, y, f);
       // the wave's frame (one tile per wave): its camera is read with scalar loads
       const GpuCamera& cam = fv.cam[__builtin_amdgcn_readfirstlane(f)];
-      pb.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
         const int set = fv.pixelSets[(size_t)y * rp.width + x];
         const int rec = set * rp.spp + s;
@@ -285,12 +284,16 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
     bool got;
     const int seg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
     const unsigned q = seg * pb.segCap + wave_append(pb.counters + qcounter_index(0, 0, seg), valid, got);
+    // the camera ray's throughput (1, 1, 1), its meta word (depth 0, unbent) and its zero
+    // radiance are implicit at depth 0: k_shade starts from them and writes pathL of every
+    // queued path, so only the paths that are not queued get their zero radiance here
     if (got) {
       pb.qPath[0][q] = p;
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
       pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
-      pb.qThr[0][q] = make_float4(1.f, 1.f, 1.f, __int_as_float((0) | (0 << 8) | (1 << 9)));
       if (pb.qTime[0]) pb.qTime[0][q] = rtime;
+    } else if (p < P) {
+      pb.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -332,6 +335,9 @@ __device__ unsigned long long g_traceProfile[8];
 #endif
 #ifndef YRT_TRI_STEP_ANY
 #define YRT_TRI_STEP_ANY YRT_TRI_STEP  // any-hit: triangles per lane per leaf step (sequential, early exit)
+#endif
+#ifndef YRT_PREFETCH_ANY
+#define YRT_PREFETCH_ANY 0  // any-hit rays refilled from prefetch registers (see k_trace)
 #endif
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
@@ -465,6 +471,23 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     q = -1;                                                                                          \
   } while (0)
   const unsigned long long ltMask = (1ull << lane) - 1ull;
+#if YRT_PREFETCH_ANY
+  // Any-hit (shadow) rays end early, so their lanes idle more (0.43 of the lanes held a ray at
+  // refill threshold 40, profiles/r02/trace_lane_utilization_r02.txt). The next 64 rays of the
+  // chunk, [next, next + 64), are loaded ahead: ray i sits in lane i mod 64. A refill takes
+  // its rays from the owning lanes (ds_bpermute) and those lanes load the ray 64 further on,
+  // so the loads overlap traversal steps instead of stalling the refill, and a lower refill
+  // threshold stops costing a memory round trip per refill.
+  constexpr bool kPrefetch = ANY && !MOTION;
+  unsigned pfLi = next + ((unsigned)(lane - (int)next) & 63u);
+  int pfQ = 0;
+  float4 pfO = make_float4(0.f, 0.f, 0.f, 0.f), pfD = pfO;
+  if (kPrefetch && pfLi < end) {
+    pfQ = qmap_phys(qm, segCap, pfLi);
+    pfO = org[pfQ];
+    pfD = dir[pfQ];
+  }
+#endif
 
 #ifdef YRT_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -481,13 +504,43 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     YRT_PROF(1, 64 - nIdle);
     if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
       if (next < end) {
+        const unsigned li = next + (unsigned)__popcll(idle & ltMask);
+#if YRT_PREFETCH_ANY
+        // shadow rays: the refill takes its rays from the prefetch registers (see pfLi)
+        int q2 = 0;
+        float4 o2 = ro, d2 = rd;
+        if constexpr (kPrefetch) {
+          const int src = (int)(li & 63u);
+          q2 = __shfl(pfQ, src, 64);
+          o2 = make_float4(__shfl(pfO.x, src, 64), __shfl(pfO.y, src, 64), __shfl(pfO.z, src, 64),
+                           __shfl(pfO.w, src, 64));
+          d2 = make_float4(__shfl(pfD.x, src, 64), __shfl(pfD.y, src, 64), __shfl(pfD.z, src, 64),
+                           __shfl(pfD.w, src, 64));
+          if (pfLi < next + (unsigned)nIdle) {
+            pfLi += 64u;
+            if (pfLi < end) {
+              pfQ = qmap_phys(qm, segCap, pfLi);
+              pfO = org[pfQ];
+              pfD = dir[pfQ];
+            }
+          }
+        }
+#endif
         if (!has) {
           if (!ANY && q >= 0) YRT_STORE_HIT();
-          const unsigned li = next + (unsigned)__popcll(idle & ltMask);
           if (li < end) {
-            q = qmap_phys(qm, segCap, li);
-            ro = org[q];
-            rd = dir[q];
+#if YRT_PREFETCH_ANY
+            if constexpr (kPrefetch) {
+              q = q2;
+              ro = o2;
+              rd = d2;
+            } else
+#endif
+            {
+              q = qmap_phys(qm, segCap, li);
+              ro = org[q];
+              rd = dir[q];
+            }
             if (MOTION) rtime = rayTime[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
@@ -780,6 +833,73 @@ __device__ __forceinline__ void post_intersect_g(const SceneView& sv, const GpuG
   }
   dg.error = fmaxf(fabsf(t), reduce_max(absv(dg.P)));
 }
+// k_shade's postIntersect: static mesh triangles read their GpuTriShade record (r0 = its
+// first 16 bytes, already loaded for the geometry id) instead of the index record and the
+// vertex arrays; the same operations as post_intersect_g on the same values, so the same bits.
+// Single triangles, moving meshes and meshes with tangent arrays take post_intersect_g.
+__device__ __forceinline__ void post_intersect_rec(const SceneView& sv, const GpuGeom& geom,
+                                                   const float4* __restrict__ rec, float4 r0, V3 org, V3 dir, float t,
+                                                   float u, float v, int gid, DG& dg, bool wantTangents, float time) {
+  if (geom.kind == GEOM_TRIANGLE || (geom.flags & (GF_MOTION | GF_TANGENT_X | GF_TANGENT_Y))) {
+    post_intersect_g(sv, geom, org, dir, t, u, v, gid, dg, wantTangents, time);
+    return;
+  }
+  dg.material = geom.material;
+  dg.light = geom.light;
+  dg.illumMask = geom.illumMask;
+  dg.shadowMask = geom.shadowMask;
+  dg.P = org + t * dir;
+  const float4 r1 = rec[1];
+  const V3 e1 = v3(r0.x, r0.y, r0.z), e2 = v3(r1.x, r1.y, r1.z);  // p0 - p1, p2 - p0
+  const float w = 1.0f - u - v;
+  const V3 dPdu = -e1, dPdv = e2;  // p1 - p0 (negation is exact), p2 - p0
+  dg.Ng = normalize(cross(e1, e2));
+  const bool meshNormals = geom.kind == GEOM_MESH_NORMALS;
+  if (meshNormals || (geom.flags & GF_NORMALS)) {
+    const float4 r2 = rec[2], r3 = rec[3], r4 = rec[4];
+    const V3 n0 = v3(r2.x, r2.y, r2.z), n1 = v3(r2.w, r3.x, r3.y), n2 = v3(r3.z, r3.w, r4.x);
+    V3 Ns = w * n0 + u * n1 + v * n2;
+    const float len2 = dot(Ns, Ns);
+    Ns = len2 > 0 ? Ns * rsqrtf_(len2) : dg.Ng;
+    if (dot(Ns, dg.Ng) < 0) Ns = -Ns;
+    dg.Ns = Ns;
+  } else {
+    dg.Ns = dg.Ng;
+  }
+  if (meshNormals) {
+    // shapes/trianglemesh_normals.cpp:125-147
+    dg.s = u;
+    dg.t = v;
+    dg.Tx = dPdu;
+    dg.Ty = dPdv;
+  } else {
+    // shapes/trianglemesh_full.cpp:192-260
+    float dsdu, dtdu, dsdv, dtdv;
+    if (geom.flags & GF_TEXCOORDS) {
+      const float4 r4 = rec[4], r5 = rec[5];
+      const float2 st0 = make_float2(r4.y, r4.z), st1 = make_float2(r4.w, r5.x), st2 = make_float2(r5.y, r5.z);
+      dg.s = st0.x * w + st1.x * u + st2.x * v;
+      dg.t = st0.y * w + st1.y * u + st2.y * v;
+      dsdu = st1.x - st0.x; dtdu = st1.y - st0.y;
+      dsdv = st2.x - st0.x; dtdv = st2.y - st0.y;
+    } else {
+      dg.s = u;
+      dg.t = v;
+      dsdu = 1; dtdu = 0;
+      dsdv = 0; dtdv = 1;
+    }
+    if (wantTangents) {
+      const V3 dPds = normalize(dPdu * dtdv - dPdv * dtdu);
+      dg.Tx = normalize(dPds - dot(dPds, dg.Ns) * dg.Ns);
+      const V3 dPdt = normalize(dPdv * dsdu - dPdu * dsdv);
+      dg.Ty = normalize(dPdt - dot(dPdt, dg.Ns) * dg.Ns);
+    } else {
+      dg.Tx = dg.Ty = v3s(0.f);
+    }
+  }
+  dg.error = fmaxf(fabsf(t), reduce_max(absv(dg.P)));
+}
+
 __device__ __forceinline__ void post_intersect(const SceneView& sv, V3 org, V3 dir, float t, float u, float v, int gid,
                                                DG& dg, bool wantTangents) {
   const int g = sv.indices[gid].w;  // geometry id rides in the index record
@@ -1071,6 +1191,22 @@ __device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, flo
 #ifndef YRT_SHADE_WAVES_ALL
 #define YRT_SHADE_WAVES_ALL 2  // the generic all-types instantiation (rare scenes): no spills at 2
 #endif
+#ifdef YRT_PATH_DEBUG
+// Debug builds only (-DYRT_PATH_DEBUG): per-vertex record of one path (pixel id, sample) of the
+// shade kernel, 32 floats per depth, laid out as oracle_debug_path's (tools/c5_path_debug.py).
+__device__ int g_dbgPath[2] = {-1, -1};
+__device__ float g_dbgTrace[32 * 32];
+extern "C" int yrt_debug_path(int pixelId, int sample, float* out) {
+  if (!out) {
+    const int v[2] = {pixelId, sample};
+    static const float z[32 * 32] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbgTrace), z, sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dbgPath), v, sizeof(v)) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbgTrace), sizeof(g_dbgTrace)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 template <unsigned MM>
 __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     MM == (YRT_ALL_MATS | YRT_ALL_LIGHTS) ? YRT_SHADE_WAVES_ALL : YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
@@ -1103,7 +1239,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
   qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
   const int n = (int)qm.pre[YRT_QSEGS];
   const int cur = depthLevel & 1;
-  const int numLights = sv.numLights;
+  const int numDirect = sv.numDirectLights;
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const unsigned ql = (unsigned)base + threadIdx.x;
     const bool active = (int)ql < n;
@@ -1136,9 +1272,18 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       org = v3(o.x, o.y, o.z);
       dir = v3(d.x, d.y, d.z);
       h = pb.hit[q];
-      const float4 t4 = pb.qThr[cur][q];
-      thr = v3(t4.x, t4.y, t4.z);
-      meta = __float_as_int(t4.w);
+      if (depthLevel == 0) {
+        // camera rays (k_raygen): throughput 1, depth 0, unbent, vacuum, zero radiance so far;
+        // pathL is written below for every queued path
+        thr = v3s(1.f);
+        meta = 1 << 9;
+        L = v3s(0.f);
+        haveL = true;
+      } else {
+        const float4 t4 = pb.qThr[cur][q];
+        thr = v3(t4.x, t4.y, t4.z);
+        meta = __float_as_int(t4.w);
+      }
       depth = meta & 255;
       ignoreVL = (meta >> 8) & 1;
       unbent = (meta >> 9) & 1;
@@ -1165,14 +1310,18 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
           const int by = max(0, min((int)(fy * (float)bp.height), bp.height - 1));
           float c[4];
           texel(bp, fv.backplateTexels, bx, by, c);
-          const float4 l4 = pb.pathL[path];
-          L = v3(l4.x, l4.y, l4.z);
-          haveL = true;
+          if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
           L = L + thr * v3(c[0], c[1], c[2]);
         } else if (!ignoreVL) {
           for (int j = 0; j < sv.numEnvLights; ++j) {
             if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
             L = L + thr * env_Le<lights_of<MM>()>(sv, sv.lights[sv.envLights[j]], wo);
+          }
+          // the zero environment lights' throughput * 0: a no-op unless the throughput is not
+          // finite, where the reference's add makes the radiance NaN
+          if (sv.numEnvZero > 0 && !(fabsf(thr.x) <= 3.40282347e38f && fabsf(thr.y) <= 3.40282347e38f && fabsf(thr.z) <= 3.40282347e38f)) {
+            if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
+            L = L + thr * v3s(0.f);
           }
         }
       }
@@ -1182,13 +1331,16 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     int g = 0;  // the hit's geometry (sv.geomRecs)
     if (active && isHit) {
       const int gid = __float_as_int(h.w);
-      g = sv.indices[gid].w;  // geometry id rides in the index record
+      const float4* tsr = (const float4*)(sv.triShade + gid);
+      const float4 r0 = tsr[0];
+      g = __float_as_int(r0.w);  // geometry id rides in the shading record
       const GpuGeomRec& gr = sv.geomRecs[g];
       const int mat = gr.g.material;
       // tangents only feed the Obj bump map and the anisotropic microfacet
       const bool wantT = mat >= 0 && (((MM & mat_bit(MAT_OBJ)) && gr.m.type == MAT_OBJ && gr.m.tex[4] >= 0) ||
                                       ((MM & mat_bit(MAT_BRUSHED_METAL)) && gr.m.type == MAT_BRUSHED_METAL));
-      post_intersect_g(sv, gr.g, org, dir, h.x, h.y, h.z, gid, dg, wantT, pb.qTime[0] ? samp(fv, 4, rec) : 0.f);
+      post_intersect_rec(sv, gr.g, tsr, r0, org, dir, h.x, h.y, h.z, gid, dg, wantT,
+                         pb.qTime[0] ? samp(fv, 4, rec) : 0.f);
       if (dot(dg.Ng, dir) > 0.f) {
         backfacing = true;
         dg.Ng = -dg.Ng;
@@ -1279,7 +1431,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
 
     // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); its
     // contribution is added to pathL[path] after the emission above (reference order)
-    for (int li = 0; li < numLights; ++li) {
+    for (int k = 0; k < numDirect; ++k) {
+      const int li = sv.directLights[k];
       bool pred = false;
       V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
       float tnear = 0.f, tfar = 0.f;
@@ -1326,10 +1479,20 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
         pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
         pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
       }
-      if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numLights + li] = sgot ? (int)si : -1;
+      if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numDirect + k] = sgot ? (int)si : -1;
       SPROF_FINE(6);  // shadow-ray append and stores
     }
     SPROF_MARK(6);  // direct light: light sample, BRDF eval, shadow-ray append and stores
+#ifdef YRT_PATH_DEBUG
+    if (active && pixelId == g_dbgPath[0] && s == g_dbgPath[1] && depth < 32) {
+      float* o = g_dbgTrace + depth * 32;
+      if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); }
+      const float r[32] = {1.f, isHit ? (float)__float_as_int(h.w) : -1.f, h.x, h.y, h.z, thr.x, thr.y, thr.z,
+                           dg.P.x, dg.P.y, dg.P.z, dg.Ns.x, dg.Ns.y, dg.Ns.z, L.x, L.y, L.z, nwi.x, nwi.y, nwi.z,
+                           spdf, sc.x, sc.y, sc.z, nthr.x, nthr.y, nthr.z, dir.x, dir.y, dir.z, org.x, (float)useDirect};
+      for (int k = 0; k < 32; ++k) o[k] = r[k];
+    }
+#endif
   }
 #ifdef YRT_SHADE_PROF
   if (threadIdx.x == 0)
@@ -1777,8 +1940,10 @@ namespace yrt {
 // rebuilt the whole Embree BVH on every face commit. Boxes stay the exact
 // union of the original vertex bounds (what the builder computes), so the hits are identical
 // to a rebuild's: the closest hit is the smallest (t, triangle id) whatever the tree.
-__global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ tris, const int4* __restrict__ indices,
+__global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ tris, GpuTriShade* __restrict__ triShade,
+                                                         const int4* __restrict__ indices,
                                                          const float4* __restrict__ positions,
+                                                         const float4* __restrict__ normals,
                                                          const int* __restrict__ leafStart,
                                                          const int* __restrict__ leafSlots, int firstTri, int numTris) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1786,6 +1951,14 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_tris(GpuTri* __restrict__ t
   const int gid = firstTri + i;
   const int4 ix = indices[gid];
   const float4 a = positions[ix.x], b = positions[ix.y], c = positions[ix.z];
+  // the shading record's edges and vertex normals (scene_gpu.cpp builds it the same way)
+  GpuTriShade& ts = triShade[gid];
+  ts.e1[0] = a.x - b.x; ts.e1[1] = a.y - b.y; ts.e1[2] = a.z - b.z;
+  ts.e2[0] = c.x - a.x; ts.e2[1] = c.y - a.y; ts.e2[2] = c.z - a.z;
+  const float4 na = normals[ix.x], nb = normals[ix.y], nc = normals[ix.z];
+  ts.n[0] = na.x; ts.n[1] = na.y; ts.n[2] = na.z;
+  ts.n[3] = nb.x; ts.n[4] = nb.y; ts.n[5] = nb.z;
+  ts.n[6] = nc.x; ts.n[7] = nc.y; ts.n[8] = nc.z;
   // every leaf slot referencing the triangle (spatial splits duplicate references)
   for (int k = leafStart[gid]; k < leafStart[gid + 1]; ++k) {
     GpuTri& t = tris[leafSlots[k]];
@@ -1834,11 +2007,12 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes(GpuNode* __restrict__
   }
 }
 
-void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* leafStart,
-                       const int* leafSlots, int firstTri, int numTris, hipStream_t s) {
+void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices, const float4* positions,
+                       const float4* normals, const int* leafStart, const int* leafSlots, int firstTri, int numTris,
+                       hipStream_t s) {
   if (numTris <= 0) return;
-  hipLaunchKernelGGL(k_refit_tris, dim3((numTris + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, tris, indices,
-                     positions, leafStart, leafSlots, firstTri, numTris);
+  hipLaunchKernelGGL(k_refit_tris, dim3((numTris + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, tris, triShade,
+                     indices, positions, normals, leafStart, leafSlots, firstTri, numTris);
 }
 
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,

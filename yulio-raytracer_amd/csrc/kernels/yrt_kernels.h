@@ -20,6 +20,7 @@ struct SceneView {
   const float2* texcoords;
   const GpuGeom* geoms;
   const GpuGeomRec* geomRecs;  // per geometry: geometry + material + tex[0] descriptor (k_shade)
+  const GpuTriShade* triShade; // per triangle: k_shade's postIntersect record
   const GpuMaterial* materials;
   const GpuTexture* textures;
   const GpuImage* images;
@@ -27,6 +28,7 @@ struct SceneView {
   const uint8_t* texQuads;  // per 8-bit texel i: texels i, i+1, i+W, i+W+1 (16 B at 4x its texel offset)
   const GpuLight* lights;
   const int* envLights;
+  const int* directLights;  // the lights whose samples can carry radiance (Device::render), in light order
   const float* hdriDist;
   const float4* media;  // medium table (transmission.rgb, eta); [0] = vacuum (materials/medium.h)
   const float4* motions;            // per vertex (moving scenes only, else null)
@@ -34,6 +36,8 @@ struct SceneView {
   const GpuTriMotion* triMotion;    // per leaf slot (moving scenes only, else null)
   int* traceSpill;   // deep traversal-stack entries: YRT_TRACE_SPILL_INTS ints
   int numLights, numEnvLights, numNodes, numTris;
+  int numDirectLights;  // k_shade's direct-light loop and the per-path shadow slots
+  int numEnvZero;       // environment lights left out of envLights: radiance exactly 0 (scene_gpu.cpp)
 };
 
 // Trace grid: 16384 blocks (swept with 128-lane blocks; with 64-lane blocks 32768 is -0.5 %),
@@ -162,8 +166,9 @@ void launch_pick(const SceneView& sv, const GpuCamera* cam, float x, float y, fl
 // BVH refit after faceCamera updates: rewrite triangles [firstTri, firstTri+numTris) (global
 // ids) from the vertex buffer in every leaf slot that references them (leafSlots[leafStart[g]
 // .. leafStart[g+1])), then refit one tree level of nodes (call deepest level first)
-void launch_refit_tris(GpuTri* tris, const int4* indices, const float4* positions, const int* leafStart,
-                       const int* leafSlots, int firstTri, int numTris, hipStream_t s);
+void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices, const float4* positions,
+                       const float4* normals, const int* leafStart, const int* leafSlots, int firstTri, int numTris,
+                       hipStream_t s);
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
                         const int* levelNodes, int count, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
