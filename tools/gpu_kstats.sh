@@ -10,7 +10,7 @@ mkdir -p $R/gpurun_out
 for d in $R/yulio-raytracer_amd/lib_variants/*/; do
   v=$(basename $d)
   [ -f $d/libdevice_singleray_mi355x.so ] || continue
-  case $v in pathdbg) continue;; esac
+  case $v in pathdbg|prof*) continue;; esac
   cd /tmp && YRT_LIB_DIR=$d timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
       -d $R/gpurun_out/ks_${TAG}_$v -o run -- python3 $R/bench.py $ARGS > $R/gpurun_out/ks_${TAG}_$v.json 2> $R/gpurun_out/ks_${TAG}_$v.err
   rc=$?

@@ -7,6 +7,10 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
+# the workload runs from /tmp: make a relative script path absolute
+S=$1; shift
+case $S in /*) ;; *) S=$R/$S;; esac
+set -- "$S" "$@"
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 cd /tmp && timeout -k 10 -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/kstats_$TAG -o run -- \
