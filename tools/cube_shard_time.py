@@ -72,9 +72,12 @@ def main():
     ap.add_argument("--size", type=int, default=1536)
     ap.add_argument("--spp", type=int, default=0, help="0: the config's own (C4 256, C5 1024)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
     a = ap.parse_args()
     spp = a.spp or (256 if a.cfg == "C4" else 1024)
     dev = yrt.Device(0)
+    if a.capacity:
+        dev.set_batch_capacity(a.capacity)
     ses = session(a.cfg, dev, a.size, spp)
     render_cube(ses, a.cfg, a.mode)  # untimed: allocations, sample table, BVH
     rows = []
@@ -83,6 +86,9 @@ def main():
         ranks = range(n) if a.ranks == "all" else [int(r) for r in a.ranks.split(",") if int(r) < n]
         times = {}
         rays = 0.0
+        if n > 1:  # untimed: the share's batch size reallocates the path queues once
+            dev.set_tile_shard(0, n)
+            render_cube(ses, a.cfg, a.mode)
         for r in ranks:
             dev.set_tile_shard(r, n)
             t = time.perf_counter()
@@ -92,7 +98,7 @@ def main():
         tmax = max(times.values())
         if n == 1:
             t1 = tmax
-        row = {"config": a.cfg, "mode": a.mode, "n": n, "ranks_timed": list(times), "ms_max": round(tmax * 1e3, 1),
+        row = {"config": a.cfg, "mode": a.mode, "capacity": a.capacity or "default", "n": n, "ranks_timed": list(times), "ms_max": round(tmax * 1e3, 1),
                "ms_mean": round(sum(times.values()) / len(times) * 1e3, 1),
                "ms_per_rank": {str(k): round(v * 1e3, 1) for k, v in times.items()},
                "predicted_efficiency": round(t1 / (n * tmax), 3) if t1 else None,

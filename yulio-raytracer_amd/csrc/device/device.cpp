@@ -58,6 +58,7 @@ struct GpuCtx {
     size_t hcWords = 0;
     bool pending = false;    // a batch was enqueued whose counters are not yet accounted
     int64_t pendTiles = 0;   // tiles done once that batch drains (progress)
+    std::vector<int64_t> pendFrameTiles;  // that batch's tiles per frame (grid-size hints)
   };
   static constexpr int kMaxLanes = 2;
   Lane lanes[kMaxLanes];
@@ -579,10 +580,29 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.fuseShadow = numDirect == 1 && !getenv("YRT_NO_SHADOW_FUSE");
       return pb;
     };
-    // queue lengths of the last drained batch per depth: grid-size hints for the next batches
-    // (batches of one frame see similar queues; -1 = no estimate yet, full grids)
-    std::vector<long long> estClosest(levels, -1), estShadow(levels, -1);
+    // grid-size hints: queue entries per tile of the drained batches, per frame and depth;
+    // a batch's hint is the sum over its frames of rate x tiles (-1 = a frame without a rate
+    // yet, full grids). Per frame because queue lengths differ between faces (sky vs floor):
+    // a cube job's batch after a face change would otherwise get another face's grids.
     const bool useHints = !getenv("YRT_NO_GRID_HINTS");
+    std::vector<double> rateC((size_t)nf * levels, -1.0), rateS((size_t)nf * levels, -1.0);
+    // the batch's tiles per frame: shard tile j of the batch is job tile index + j * count
+    auto frame_tiles = [&](int64_t firstTile, int64_t ntiles, int64_t* per) {
+      for (int f = 0; f < nf; ++f) per[f] = 0;
+      const int64_t tpf = rp.tilesPerFrame;
+      int64_t j = firstTile;
+      const int64_t jEnd = firstTile + ntiles;
+      while (j < jEnd) {
+        const int64_t f = (index + j * count) / tpf;
+        // last j whose tile is still in frame f: index + j * count < (f + 1) * tpf
+        int64_t jLast = ((f + 1) * tpf - 1 - index) / count;
+        if (jLast >= jEnd) jLast = jEnd - 1;
+        per[f] += jLast - j + 1;
+        j = jLast + 1;
+      }
+    };
+    std::vector<int64_t> curTiles(nf);
+    std::vector<long long> estClosest(levels, -1), estShadow(levels, -1);
     auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + 65536; };
     // waits for the lane's previous batch and accounts its queue counters
     int64_t tilesDone = 0;
@@ -595,8 +615,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           nc += L.hc[qcounter_index(d, 0, k)];
           ns += L.hc[qcounter_index(d, 1, k)];
         }
-        estClosest[d] = (long long)nc;
-        estShadow[d] = (long long)ns;
+        // the batch's rate per tile, credited to each of its frames
+        for (int f = 0; f < nf; ++f)
+          if (L.pendFrameTiles[f]) {
+            rateC[(size_t)f * levels + d] = nc / (double)L.pendTiles;
+            rateS[(size_t)f * levels + d] = ns / (double)L.pendTiles;
+          }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           g.stats.raysClosest += nc;
           if (nc) g.stats.launchesClosest += 1;
@@ -625,6 +649,20 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
       bi.tileStride = count;
       bi.tileOffset = index;
+      frame_tiles(first, bi.numPixels / 256, curTiles.data());
+      for (int d = 0; d < levels; ++d) {
+        double ec = 0, es = 0;
+        bool known = true;
+        for (int f = 0; f < nf && known; ++f) {
+          if (!curTiles[f]) continue;
+          const double rc = rateC[(size_t)f * levels + d], rs = rateS[(size_t)f * levels + d];
+          known = rc >= 0;
+          ec += rc * (double)curTiles[f];
+          es += rs * (double)curTiles[f];
+        }
+        estClosest[d] = known ? (long long)ec : -1;
+        estShadow[d] = known ? (long long)es : -1;
+      }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
       launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
@@ -659,6 +697,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipMemcpyAsync(L.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       L.pending = true;
       L.pendTiles = bi.numPixels / 256;
+      L.pendFrameTiles.assign(curTiles.begin(), curTiles.end());
     }
     for (int l = 0; l < nl; ++l) drain(g.lanes[l]);
     for (auto& e : evs) {

@@ -336,9 +336,6 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_TRI_STEP_ANY
 #define YRT_TRI_STEP_ANY YRT_TRI_STEP  // any-hit: triangles per lane per leaf step (sequential, early exit)
 #endif
-#ifndef YRT_PREFETCH_ANY
-#define YRT_PREFETCH_ANY 0  // any-hit rays refilled from prefetch registers (see k_trace)
-#endif
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
@@ -471,23 +468,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     q = -1;                                                                                          \
   } while (0)
   const unsigned long long ltMask = (1ull << lane) - 1ull;
-#if YRT_PREFETCH_ANY
-  // Any-hit (shadow) rays end early, so their lanes idle more (0.43 of the lanes held a ray at
-  // refill threshold 40, profiles/r02/trace_lane_utilization_r02.txt). The next 64 rays of the
-  // chunk, [next, next + 64), are loaded ahead: ray i sits in lane i mod 64. A refill takes
-  // its rays from the owning lanes (ds_bpermute) and those lanes load the ray 64 further on,
-  // so the loads overlap traversal steps instead of stalling the refill, and a lower refill
-  // threshold stops costing a memory round trip per refill.
-  constexpr bool kPrefetch = ANY && !MOTION;
-  unsigned pfLi = next + ((unsigned)(lane - (int)next) & 63u);
-  int pfQ = 0;
-  float4 pfO = make_float4(0.f, 0.f, 0.f, 0.f), pfD = pfO;
-  if (kPrefetch && pfLi < end) {
-    pfQ = qmap_phys(qm, segCap, pfLi);
-    pfO = org[pfQ];
-    pfD = dir[pfQ];
-  }
-#endif
 
 #ifdef YRT_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -505,42 +485,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
       if (next < end) {
         const unsigned li = next + (unsigned)__popcll(idle & ltMask);
-#if YRT_PREFETCH_ANY
-        // shadow rays: the refill takes its rays from the prefetch registers (see pfLi)
-        int q2 = 0;
-        float4 o2 = ro, d2 = rd;
-        if constexpr (kPrefetch) {
-          const int src = (int)(li & 63u);
-          q2 = __shfl(pfQ, src, 64);
-          o2 = make_float4(__shfl(pfO.x, src, 64), __shfl(pfO.y, src, 64), __shfl(pfO.z, src, 64),
-                           __shfl(pfO.w, src, 64));
-          d2 = make_float4(__shfl(pfD.x, src, 64), __shfl(pfD.y, src, 64), __shfl(pfD.z, src, 64),
-                           __shfl(pfD.w, src, 64));
-          if (pfLi < next + (unsigned)nIdle) {
-            pfLi += 64u;
-            if (pfLi < end) {
-              pfQ = qmap_phys(qm, segCap, pfLi);
-              pfO = org[pfQ];
-              pfD = dir[pfQ];
-            }
-          }
-        }
-#endif
         if (!has) {
           if (!ANY && q >= 0) YRT_STORE_HIT();
           if (li < end) {
-#if YRT_PREFETCH_ANY
-            if constexpr (kPrefetch) {
-              q = q2;
-              ro = o2;
-              rd = d2;
-            } else
-#endif
-            {
-              q = qmap_phys(qm, segCap, li);
-              ro = org[q];
-              rd = dir[q];
-            }
+            q = qmap_phys(qm, segCap, li);
+            ro = org[q];
+            rd = dir[q];
             if (MOTION) rtime = rayTime[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
