@@ -13,6 +13,8 @@ is the slowest share; efficiency = T(1) / (N * T(N)).
 
 --mode face: one rtRenderFrame per face (the reference's loop);
 --mode cube: the 12 faces in one yrtRenderFrames call (tiles of all faces in one sequence).
+Times are render-only: each call writes its frames back into the session's host framebuffers
+(as the product does) but the images are not converted to numpy arrays.
 
 usage: python tools/cube_shard_time.py C4|C5 [--mode face|cube] [--gpus 1,2,4,8] [--ranks all|0]
        [--spp N] [--size S]
@@ -45,19 +47,21 @@ def session(cfg, dev, size, spp):
 def render_cube(ses, cfg, mode):
     """One full cubemap; returns rays traced (closest + shadow)."""
     dev = ses.device
+    # render only: the frames are written back into the session's (host) framebuffers as the
+    # product does, but not converted to numpy here
     if mode == "cube":
         if cfg == "C4":
-            ses.render_cube()
+            ses.render_cube(read=False)
         else:
-            ses.render_scene_cube(0)
+            ses.render_scene_cube(0, read=False)
         st = dev.render_stats()
         return st["raysClosest"] + st["raysShadow"]
     rays = 0.0
     for f in range(12):
         if cfg == "C4":
-            ses.render(f)
+            ses.render(f, read=False)
         else:
-            ses.render_scene_camera(f)
+            ses.render_scene_camera(f, read=False)
         st = dev.render_stats()
         rays += st["raysClosest"] + st["raysShadow"]
     return rays

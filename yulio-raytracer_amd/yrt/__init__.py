@@ -463,14 +463,17 @@ class Session:
             raise RuntimeError(N.fe.yrtFrontendLastError().decode())
         return h
 
-    def render(self, face=-1):
-        """Renders one frame (mono face=-1, stereo cube face 0..11) and returns it as numpy."""
+    def render(self, face=-1, read=True):
+        """Renders one frame (mono face=-1, stereo cube face 0..11) and returns it as numpy
+        (None when read=False: the frame stays in the session's framebuffer)."""
         p = N.fe.yrtSessionRender(self.h, face)
         if not p:
             raise RuntimeError(N.fe.yrtFrontendLastError().decode())
         i = self.info()
-        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[i["framebufferFormat"]]
         N.dev.yrtUnmapFrameBuffer(self.device.h, i["framebuffer"], -1)
+        if not read:
+            return None
+        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[i["framebufferFormat"]]
         return self.device.framebuffer_array(i["framebuffer"], i["width"], i["height"], fmt)
 
     def _cube_faces(self):
@@ -511,14 +514,17 @@ class Session:
             raise RuntimeError(N.fe.yrtFrontendLastError().decode())
         return h
 
-    def render_scene_camera(self, i):
-        """One FPR face (faceCamera update, scene commit, render) of scene camera i."""
+    def render_scene_camera(self, i, read=True):
+        """One FPR face (faceCamera update, scene commit, render) of scene camera i (numpy, or
+        None when read=False)."""
         p = N.fe.yrtSessionRenderSceneCamera(self.h, i)
         if not p:
             raise RuntimeError(N.fe.yrtFrontendLastError().decode())
         info = self.info()
-        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[info["framebufferFormat"]]
         N.dev.yrtUnmapFrameBuffer(self.device.h, info["framebuffer"], -1)
+        if not read:
+            return None
+        fmt = ("RGB8", "RGBA8", "RGB_FLOAT32", "RGBA_FLOAT32")[info["framebufferFormat"]]
         return self.device.framebuffer_array(info["framebuffer"], info["width"], info["height"], fmt)
 
     def output(self, file=None):
