@@ -42,3 +42,18 @@ def test_sample_scene_parity(gpu_device, name, face):
     # GPU must give them on the same pixels
     parity(img, ref, 0.999, nan_ok=name == "test_transmissive")
     s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("face", [0, 5])
+def test_zero_radiance_lights_parity(gpu_device, face):
+    """A second dome light with L = 0 0 0 on the transmissive scene: the device leaves it out of
+    the direct-light and miss loops (its terms are exactly 0), but a path whose throughput is
+    already NaN (this scene's ThinDielectric log(0) * 0) must still turn NaN at a miss, as the
+    reference's `L += throughput * 0` does. Bit-exact against the oracle, NaN masks included."""
+    s = yrt.Session(SCENES_ARGS["test_transmissive"] + ["-ambientlight", "0", "0", "0", "-size", "64", "64", "-spp",
+                                                        "4", "-fb", "RGB_FLOAT32"], device=gpu_device)
+    img = s.render(face)
+    ref, _ = oracle.render(s.export_frame(face), 64, 64, s.info()["gamma"])
+    parity(img, ref, 0.999, nan_ok=True)
+    s.close()
