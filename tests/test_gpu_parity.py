@@ -389,3 +389,27 @@ def test_startrt_multi_device_equals_single(tmp_path, monkeypatch):
         assert yrt.GetLastErrorRT() == 0
         outs.append([(d / f"room_{n}.jpg").read_bytes() for n in ("Kitchen", "Hall")])
     assert outs[0] == outs[1]
+
+
+def test_debug_pixel_samples_match_oracle(gpu_device):
+    """yrtDebugPixelSamples (the parity-debugging capture): the per-sample radiance of one pixel,
+    in the pixel's summation order, equals the oracle's per-sample radiance bit for bit; the
+    capture disarms, and reading without an armed capture on a fresh device raises."""
+    s = yrt.Session(c2_args(64, 16) + ["-fb", "RGB_FLOAT32"], device=gpu_device)
+    x, y = 37, 22
+    gpu_device.debug_pixel_arm(x, y, 64, 0, 16)
+    try:
+        s.render()
+        g = gpu_device.debug_pixel_samples(16)
+    finally:
+        gpu_device.debug_pixel_arm(-1, 0, 64)
+    o = oracle.debug_pixel(s.export_frame(), 64, 64, x, y)
+    assert g.shape == o.shape == (16, 3)
+    assert np.array_equal(g, o)
+    s.close()
+    fresh = yrt.Device(0)
+    try:
+        with pytest.raises(RuntimeError):
+            fresh.debug_pixel_samples(4)
+    finally:
+        fresh.close()

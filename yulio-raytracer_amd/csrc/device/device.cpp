@@ -198,7 +198,10 @@ class Device {
     stream = ctx[0]->stream;
     HIP_CHECK(hipSetDevice(hipDevice));
   }
+  DevBuf dbgPixelBuf;   // yrtDebugPixelSamples capture (a debugging aid), armed on this device
+  int dbgPixelCap = 0;
   ~Device() {
+    if (dbgPixelBuf.p) (void)debug_pixel_capture(-1, -1, nullptr);  // no kernel may write it once freed
     for (auto* h : handles) delete h;
     handles.clear();
     try {
@@ -1663,17 +1666,18 @@ int yrtDebugPixelSamples(YRTDevice dev, int pixelId, int frame, float* out4, int
   Device& D = *dev->d;
   if (!D.gpu) throw std::runtime_error("host-only device");
   HIP_CHECK(hipSetDevice(D.hipDevice));
-  static DevBuf buf;  // one capture per process (a debugging aid)
-  static int capacity = 0;
+  // one capture at a time per process (the kernel-side target is a module global)
+  DevBuf& buf = D.dbgPixelBuf;
   if (!out4) {
     if (pixelId < 0) return debug_pixel_capture(-1, -1, nullptr);
     if (maxSamples < 1) throw std::runtime_error("yrtDebugPixelSamples: maxSamples < 1");
     buf.alloc((size_t)maxSamples * sizeof(float4));
     HIP_CHECK(hipMemset(buf.p, 0, (size_t)maxSamples * sizeof(float4)));
-    capacity = maxSamples;
+    D.dbgPixelCap = maxSamples;
     return debug_pixel_capture(pixelId, frame, buf.as<float4>());
   }
-  const int n = std::min(maxSamples, capacity);
+  if (!buf.p) throw std::runtime_error("yrtDebugPixelSamples: no capture armed on this device");
+  const int n = std::min(maxSamples, D.dbgPixelCap);
   HIP_CHECK(hipDeviceSynchronize());
   HIP_CHECK(hipMemcpy(out4, buf.p, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
   return n;
