@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Phase breakdown of k_shade on the C3 stand-in (needs a -DYRT_SHADE_PROF build, selected with
-YRT_LIB_DIR): shader-clock cycles per phase summed over the waves of every shade launch of one
-frame. usage: YRT_LIB_DIR=... python tools/shade_profile.py [size] [spp]"""
+"""Phase breakdown of k_shade on the C3 stand-in or a C4 stereo face (needs a -DYRT_SHADE_PROF
+build, selected with YRT_LIB_DIR): shader-clock cycles per phase summed over the waves of every
+shade launch of one frame.
+usage: YRT_LIB_DIR=... python tools/shade_profile.py [C3|C4] [size] [spp] [fine]"""
 import ctypes as C
 import sys
 from pathlib import Path
@@ -10,7 +11,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT), str(ROOT / "yulio-raytracer_amd"), str(ROOT / "tests")]
 import yrt  # noqa: E402
 from yrt import _native as N  # noqa: E402
-from helpers import c3_args  # noqa: E402
+from helpers import c3_args, c4_args  # noqa: E402
 
 PHASES = ["queue record + pixel/sample record", "misses (env/backplate)", "postIntersect",
           "material shade + emission", "continuation sample", "continuation append/stores",
@@ -18,13 +19,15 @@ PHASES = ["queue record + pixel/sample record", "misses (env/backplate)", "postI
 FINE = ["record .. RR (before BRDF sample)", "CompositedBRDF::sample", "rest of continuation + append",
         "Light::sample", "CompositedBRDF::eval", "jitter + contribution", "shadow append + stores",
         "loop overhead"]
-if len(sys.argv) > 3 and sys.argv[3] == "fine":  # a -DYRT_SHADE_PROF=2 build
+argv = sys.argv[1:]
+cfg = argv.pop(0) if argv and argv[0] in ("C3", "C4") else "C3"
+if len(argv) > 2 and argv[2] == "fine":  # a -DYRT_SHADE_PROF=2 build
     PHASES = FINE
 
-size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-spp = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+size = int(argv[0]) if len(argv) > 0 else 1024
+spp = int(argv[1]) if len(argv) > 1 else 16
 dev = yrt.Device(0)
-s = yrt.Session(c3_args(size, spp), device=dev)
+s = yrt.Session((c4_args if cfg == "C4" else c3_args)(size, spp), device=dev)
 dev.set_kernel_timing(True)
 s.render()  # warm-up
 buf = (C.c_uint64 * 8)()
@@ -37,6 +40,6 @@ if rc != 0:
     sys.exit("not a YRT_SHADE_PROF build")
 tot = sum(v)
 items = st["raysClosest"]
-print(f"C3 {size}^2 {spp}spp: shade items {items:.0f}, shade ms {st['msShade']:.1f}")
+print(f"{cfg} {size}^2 {spp}spp: shade items {items:.0f}, shade ms {st['msShade']:.1f}")
 for name, x in zip(PHASES, v):
     print(f"  {name:38s} {100.0 * x / tot:6.2f} %   {x / max(items, 1) * 64:9.1f} wave-cycles per 64 items")

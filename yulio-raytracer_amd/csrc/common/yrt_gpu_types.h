@@ -147,6 +147,23 @@ struct GpuLight {
   int32_t hdriW, hdriH, pad2[2];
 };
 
+// Division of n in [0, 2^31) by a run-time constant d in [1, 2^31) as multiply-high, add and
+// shift (the round-up method of Granlund & Montgomery, PLDI 1994): q = (umulhi(n, mul) + n) >>
+// shift, three VALU instead of the ~25 of an integer division. Exact over the whole range
+// (tests/test_fastdiv.py checks the construction).
+struct FastDiv {
+  uint32_t mul, shift;
+};
+static inline FastDiv fastdiv_make(uint32_t d) {
+  uint32_t shift = 0;
+  while (shift < 31 && (1u << shift) < d) ++shift;
+  const uint64_t magic = ((uint64_t)1 << 32) * (((uint64_t)1 << shift) - d) / d + 1;
+  FastDiv f;
+  f.mul = (uint32_t)magic;
+  f.shift = shift;
+  return f;
+}
+
 // Renderer parameters (integrators/pathtraceintegrator.cpp:21-33 defaults).
 struct GpuRenderParams {
   int32_t maxDepth, rrDepth, spp, sets;
@@ -160,6 +177,7 @@ struct GpuRenderParams {
   // frames rendered together (yrtRenderFrames: the 12 faces of a stereo cubemap): tile t of
   // the job is tile t % tilesPerFrame of frame t / tilesPerFrame (numTilesX * numTilesY each)
   int32_t numFrames, tilesPerFrame, pad;
+  FastDiv divTilesX, divTilesPerFrame;  // fastdiv_make(numTilesX), fastdiv_make(tilesPerFrame)
 };
 
 // Camera (cameras/pinholecamera.h:15-21, cameras/StereoCubeCamera.h:16-65).
@@ -171,6 +189,17 @@ struct GpuCamera {
   float p2w[6][12];           // pixel2world[face]: vx, vy, vz, p (column-major)
   float origin[4], up[4], xyzStraight[4];
   float eyeSeparation, rcpZeroParallaxDistance, falloffAngle, pad2;
+  // CAM_STEREO without toe-in: the terms of StereoCubeCamera::ray that do not depend on the
+  // pixel, computed on the host with the device's operations (objects.cpp stereo_precompute):
+  //   lin[f]   (pixel2world[f] * translate(eyeOffset, 0, 0)).l = pixel2world[f].l * identity
+  //   zero[f]  the translation's zero products of that point, (0 * vy) + (0 * vz), per axis
+  //   rot      normalize(up) as in l3_rotate: u.xyz, then u.x*u.x, 1-u.x*u.x, u.y*u.y,
+  //            1-u.y*u.y, u.z*u.z, 1-u.z*u.z, u.x*u.y, u.x*u.z, u.y*u.z
+  //   negO     -origin;  rotP  (translate(origin) * rotate(up, theta)).p = I*0 + origin
+  float lin[6][9];
+  float zero[6][3];
+  float rot[12];
+  float negO[4], rotP[4];
 };
 
 // Precomputed sample table (samplers/sampler.cpp:85-158), SoA [dim][set*spp + s].

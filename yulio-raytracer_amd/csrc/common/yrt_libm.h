@@ -151,11 +151,21 @@ YRT_LIBM_FN float yrt_asinf(float x) {
   const float r = yrt_lm_asin_core(x < 0.0f ? -x : x);
   return x < 0.0f ? -r : r;
 }
+/* acos: x < -1/2: pi - 2 asin(sqrt((1+x)/2)); x > 1/2: 2 asin(sqrt((1-x)/2)); else
+   pi/2 - asin(x). Every range's asin argument is <= 1/2 (the core's polynomial branch), so the
+   three ranges select one argument and share one sqrt and one polynomial: a wave whose lanes
+   span the ranges evaluates the core once instead of once per range. */
 YRT_LIBM_FN float yrt_acosf(float x) {
   if (!(x >= -1.0f && x <= 1.0f)) return yrt_lm_float(0x7fc00000u);
-  if (x < -0.5f) return 3.14159265358979323846f - 2.0f * yrt_lm_asin_core(yrt_lm_sqrt(0.5f * (1.0f + x)));
-  if (x > 0.5f) return 2.0f * yrt_lm_asin_core(yrt_lm_sqrt(0.5f * (1.0f - x)));
-  return 1.5707963267948966192f - yrt_asinf(x);
+  const int lo = x < -0.5f, hi = x > 0.5f;
+  const float w = yrt_lm_sqrt(0.5f * (hi ? 1.0f - x : 1.0f + x));
+  const float a = (lo || hi) ? w : (x < 0.0f ? -x : x);
+  const float z = a * a;
+  const float r = ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+                   1.6666752422e-1f) * z * a + a;
+  if (lo) return 3.14159265358979323846f - 2.0f * r;
+  if (hi) return 2.0f * r;
+  return 1.5707963267948966192f - (x < 0.0f ? -r : r);
 }
 
 /* ---- atan / atan2 */

@@ -412,6 +412,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   rp.numPrecomp = (int)G.precomputed.size();
   rp.numFrames = nf;
   rp.tilesPerFrame = rp.numTilesX * rp.numTilesY;
+  rp.divTilesX = fastdiv_make((uint32_t)rp.numTilesX);
+  rp.divTilesPerFrame = fastdiv_make((uint32_t)rp.tilesPerFrame);
 
   // samples: PathTraceIntegrator::requestSamples (pathtraceintegrator.cpp:35-47)
   SampleRequest req;
@@ -652,6 +654,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
       bi.tileStride = count;
       bi.tileOffset = index;
+      bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
       frame_tiles(first, bi.numPixels / 256, curTiles.data());
       for (int d = 0; d < levels; ++d) {
         double ec = 0, es = 0;

@@ -545,6 +545,22 @@ void CameraObj::commit() {
     cam.origin[0] = origin.x; cam.origin[1] = origin.y; cam.origin[2] = origin.z;
     cam.up[0] = up.x; cam.up[1] = up.y; cam.up[2] = up.z;
     cam.xyzStraight[0] = xyz.x; cam.xyzStraight[1] = xyz.y; cam.xyzStraight[2] = xyz.z;
+    // the pixel-independent terms of StereoCubeCamera::ray (StereoCubeCamera.h:142-159), with
+    // the same operations the per-ray code would run (GpuCamera::lin ... rotP)
+    for (int i = 0; i < 6; ++i) {
+      const L3 lin = mul(p2w[i].l, l3_identity());  // (p2w * translate(eyeOffset,0,0)).l
+      const float v[9] = {lin.vx.x, lin.vx.y, lin.vx.z, lin.vy.x, lin.vy.y, lin.vy.z, lin.vz.x, lin.vz.y, lin.vz.z};
+      memcpy(cam.lin[i], v, sizeof(v));
+      const V3 z = 0.f * p2w[i].l.vy + 0.f * p2w[i].l.vz;  // the translation's zero products
+      cam.zero[i][0] = z.x; cam.zero[i][1] = z.y; cam.zero[i][2] = z.z;
+    }
+    const V3 u = normalize(up);  // l3_rotate (common/math/linearspace3.h rotate)
+    const float rot[12] = {u.x,     u.y,           u.z,     u.x * u.x, 1 - u.x * u.x, u.y * u.y,
+                           1 - u.y * u.y, u.z * u.z, 1 - u.z * u.z, u.x * u.y, u.x * u.z, u.y * u.z};
+    memcpy(cam.rot, rot, sizeof(rot));
+    const V3 rotP = mul(l3_identity(), v3s(0.0f)) + origin;  // (translate(origin) * rotate).p
+    cam.negO[0] = -origin.x; cam.negO[1] = -origin.y; cam.negO[2] = -origin.z;
+    cam.rotP[0] = rotP.x; cam.rotP[1] = rotP.y; cam.rotP[2] = rotP.z;
   } else {
     throw std::runtime_error("camera type '" + type + "' is outside the MI355X device's scope");
   }

@@ -72,6 +72,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   std::vector<GpuLight> lights;
   std::vector<int> envLights;
   int numEnvZero = 0;
+  int numEnvDir = 0;
   std::map<const MaterialInst*, int> matIds;
   std::map<const TextureInst*, int> texIds;
   std::map<const ImageObj*, int> imgIds;
@@ -168,8 +169,12 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
         const float* f = (const float*)L.image->data.data();
         for (size_t k = 0; k < L.image->data.size() / 4 && zero; ++k) zero = std::isfinite(f[k]);
       }
-      if (zero) ++numEnvZero;
-      else envLights.push_back((int)lights.size());
+      if (zero) {
+        ++numEnvZero;
+      } else {
+        envLights.push_back((int)lights.size());
+        if (L.type != LIGHT_AMBIENT) ++numEnvDir;
+      }
     }
     if (L.type == LIGHT_HDRI) {
       g.image = imageId(L.image);
@@ -394,6 +399,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   S->view.numLights = (int)lights.size();
   S->view.numEnvLights = (int)envLights.size();
   S->view.numEnvZero = numEnvZero;
+  S->view.numEnvDir = numEnvDir;
   S->view.numNodes = (int)bvh.nodes.size();
   S->view.numTris = gidBase;
   bind_view(*S);

@@ -141,9 +141,20 @@ __device__ __forceinline__ float hash_u01(uint32_t seed, uint32_t pixel, uint32_
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
-__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+// Records every lane of a wave reads at one address (the render parameters, the frame's
+// camera) are read through the constant address space: scalar loads into SGPRs instead of
+// per-lane vector loads held in VGPRs (the kernels never write them).
+#define YRT_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const YRT_CONST T& const_ref(const T* p) {
+  return *(const YRT_CONST T*)p;
+}
+
+template <class F>
+__device__ __forceinline__ V3 ld3(const F* p) { return v3(p[0], p[1], p[2]); }
 __device__ __forceinline__ V3 ld3(const float4& p) { return v3(p.x, p.y, p.z); }
-__device__ __forceinline__ A3 ldA3(const float* m) {
+template <class F>
+__device__ __forceinline__ A3 ldA3(const F* m) {
   return a3(l3(v3(m[0], m[1], m[2]), v3(m[3], m[4], m[5]), v3(m[6], m[7], m[8])), v3(m[9], m[10], m[11]));
 }
 
@@ -151,7 +162,8 @@ __device__ __forceinline__ A3 ldA3(const float* m) {
 // PinHoleCamera::ray (cameras/pinholecamera.h:23-25)
 // StereoCubeCamera::ray (cameras/StereoCubeCamera.h:68-161)
 // DepthOfFieldCamera::ray (cameras/depthoffieldcamera.h:20-26); (lx, ly) = the lens sample
-__device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3& dir, float lx = 0.f,
+template <class CAM>  // GpuCamera, or a YRT_CONST one (scalar loads)
+__device__ void camera_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir, float lx = 0.f,
                            float ly = 0.f) {
   if (cam.type == CAM_PINHOLE) {
     A3 p2w = ldA3(cam.p2w[0]);
@@ -197,37 +209,70 @@ __device__ void camera_ray(const GpuCamera& cam, float fx, float fy, V3& org, V3
     const float coef = 1.f - smoothstepf(0.f, 1.f, smoothstepf(cam.falloffAngle, 90.f, absoluteVerticalAngle));
     eyeOffset *= coef;
   }
-  p2w = mul(p2w, a3_translate(v3(eyeOffset, 0.f, 0.f)));
-  const V3 origin = ld3(cam.origin), up = ld3(cam.up);
-  const A3 rayRotationSpace = a3_rotate_about(origin, up, theta);
-  const V3 rayOrigin = mul(rayRotationSpace, p2w).p;
   if (cam.toeIn) {
+    p2w = mul(p2w, a3_translate(v3(eyeOffset, 0.f, 0.f)));
+    const V3 origin = ld3(cam.origin), up = ld3(cam.up);
+    const A3 rayRotationSpace = a3_rotate_about(origin, up, theta);
+    const V3 rayOrigin = mul(rayRotationSpace, p2w).p;
     const float toeInCorrection = -yrt_atanf(eyeOffset * cam.rcpZeroParallaxDistance);
     p2w = mul(a3_rotate_about(rayOrigin, up, toeInCorrection), p2w);
+    org = rayOrigin;
+    dir = normalize(fx * p2w.l.vx + yPixel * p2w.l.vy + p2w.l.vz);
+    return;
   }
-  org = rayOrigin;
-  dir = normalize(fx * p2w.l.vx + yPixel * p2w.l.vy + p2w.l.vz);
+  // Without toe-in the same products with the pixel-independent terms taken from the camera
+  // record (objects.cpp): translate(origin) * rotate(up, theta) * translate(-origin) has the
+  // rotation as its linear part (the identity factors' ones and zeros only add exact zeros),
+  // and its point is rotation * (-origin) + rotP; the shifted eye point is
+  // p2w.p + eyeOffset * p2w.vx plus the translation's zero products.
+  const auto* R = cam.rot;  // u.xyz, uxx, 1-uxx, uyy, 1-uyy, uzz, 1-uzz, uxy, uxz, uyz
+  const float sn = yrt_sinf(theta), cs = yrt_cosf(theta), omc = 1 - cs;
+  const V3 rvx = v3(R[3] + R[4] * cs, R[9] * omc + R[2] * sn, R[10] * omc - R[1] * sn);
+  const V3 rvy = v3(R[9] * omc - R[2] * sn, R[5] + R[6] * cs, R[11] * omc + R[0] * sn);
+  const V3 rvz = v3(R[10] * omc + R[1] * sn, R[11] * omc - R[0] * sn, R[7] + R[8] * cs);
+  const V3 bp = (cam.negO[0] * rvx + cam.negO[1] * rvy + cam.negO[2] * rvz) + ld3(cam.rotP);
+  const auto* z = cam.zero[eyeCubeFaceIndex];
+  const V3 eye = v3(eyeOffset * p2w.l.vx.x + z[0], eyeOffset * p2w.l.vx.y + z[1], eyeOffset * p2w.l.vx.z + z[2]) + p2w.p;
+  org = (eye.x * rvx + eye.y * rvy + eye.z * rvz) + bp;
+  const auto* m = cam.lin[eyeCubeFaceIndex];
+  dir = normalize(fx * v3(m[0], m[1], m[2]) + yPixel * v3(m[3], m[4], m[5]) + v3(m[6], m[7], m[8]));
 }
 
 // ---------------------------------------------------------------- batch pixel mapping
 // Batch pixel i -> (frame f, pixel x, y). A batch holds whole 16x16 tiles of the job's tile
 // sequence (all frames' tiles, frame-major); the 256 pixels of a tile are consecutive, so the
 // 64 lanes of a wave (64-aligned i) always share the tile and the frame.
-__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y,
-                                            int& f) {
-  int tile = bi.tileOffset + (bi.firstTile + (i >> 8)) * bi.tileStride;
-  const int within = i & 255;
+template <class D>  // FastDiv, or a YRT_CONST one
+__device__ __forceinline__ int fastdiv(int n, const D& d) {  // n in [0, 2^31)
+  return (int)((__umulhi((unsigned)n, d.mul) + (unsigned)n) >> d.shift);
+}
+// the tile of batch-pixel block ib = i >> 8: its frame and first pixel (false past the job)
+template <class RP>
+__device__ __forceinline__ bool batch_tile(const RP& rp, const BatchInfo& bi, int ib, int& x0, int& y0,
+                                           int& f) {
+  int tile = bi.tileOffset + (bi.firstTile + ib) * bi.tileStride;
   f = 0;
   if (tile >= rp.tilesPerFrame * rp.numFrames) return false;
   if (rp.numFrames > 1) {
-    f = tile / rp.tilesPerFrame;
+    f = fastdiv(tile, rp.divTilesPerFrame);
     tile -= f * rp.tilesPerFrame;
   }
-  x = (tile % rp.numTilesX) * 16 + (within & 15);
-  y = (tile / rp.numTilesX) * 16 + (within >> 4);
+  const int ty = fastdiv(tile, rp.divTilesX);
+  x0 = (tile - ty * rp.numTilesX) * 16;
+  y0 = ty * 16;
+  return true;
+}
+template <class RP>
+__device__ __forceinline__ bool batch_pixel(const RP& rp, const BatchInfo& bi, int i, int& x, int& y,
+                                            int& f) {
+  int x0 = 0, y0 = 0;
+  if (!batch_tile(rp, bi, i >> 8, x0, y0, f)) return false;
+  x = x0 + (i & 15);
+  y = y0 + ((i >> 4) & 15);
   return x < rp.width && y < rp.height;
 }
-__device__ __forceinline__ bool batch_pixel(const GpuRenderParams& rp, const BatchInfo& bi, int i, int& x, int& y) {
+template <class RP>
+__device__ __forceinline__ bool batch_pixel(const RP& rp, const BatchInfo& bi, int i, int& x, int& y) {
   int f;
   return batch_pixel(rp, bi, i, x, y, f);
 }
@@ -257,7 +302,8 @@ __global__ void k_pixel_sets(const GpuRenderParams* __restrict__ rpp, uint8_t* _
 }
 
 __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers pb, BatchInfo bi) {
-  const GpuRenderParams& rp = *fv.rp;
+  static_assert(YRT_BLOCK <= 256 && 256 % YRT_BLOCK == 0, "a raygen block lies in one 256-pixel tile");
+  const YRT_CONST GpuRenderParams& rp = const_ref(fv.rp);
   const int P = bi.numPixels * rp.spp;
   for (int base = blockIdx.x * blockDim.x; base < P; base += gridDim.x * blockDim.x) {
     const int p = base + threadIdx.x;
@@ -265,11 +311,14 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
     V3 org = v3s(0.f), dir = v3s(0.f);
     float rtime = 0.f;
     if (p < P) {  // P and numPixels are multiples of 256: whole waves are in or out
-      const int s = p / bi.numPixels, i = p - s * bi.numPixels;
-      int x, y, f;
-      valid = batch_pixel(rp, bi, i, x, y, f);
-      // the wave's frame (one tile per wave): its camera is read with scalar loads
-      const GpuCamera& cam = fv.cam[__builtin_amdgcn_readfirstlane(f)];
+      // the block's paths share the sample index, the tile and the frame (numPixels is a
+      // multiple of 256): computed once from the block base, on the scalar unit
+      const int s = fastdiv(base, bi.divPixels);
+      int x0 = 0, y0 = 0, f = 0;
+      const bool tileOk = batch_tile(rp, bi, (base - s * bi.numPixels) >> 8, x0, y0, f);
+      const int x = x0 + (p & 15), y = y0 + ((p >> 4) & 15);
+      valid = tileOk && x < rp.width && y < rp.height;
+      const YRT_CONST GpuCamera& cam = const_ref(fv.cam + f);  // scalar loads
       if (valid) {
         const int set = fv.pixelSets[(size_t)y * rp.width + x];
         const int rec = set * rp.spp + s;
@@ -1183,7 +1232,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
 #else
 #define SPROF_FINE(k) ((void)0)
 #endif
-  const GpuRenderParams& rp = *fv.rp;
+  const YRT_CONST GpuRenderParams& rp = const_ref(fv.rp);
   __shared__ QMap qm;
   __shared__ float sstash[7 * YRT_MAX_COMPS * YRT_BLOCK];  // set_sample candidates, [slot][lane]
   qmap_load(qm, pb.counters + qcounter_index(depthLevel, 0, 0), YRT_QSEGS);
@@ -1218,9 +1267,6 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     SPROF_FINE(7);
     if (active) {
       path = pb.qPath[cur][q];
-      const float4 o = pb.qOrg[cur][q], d = pb.qDir[cur][q];
-      org = v3(o.x, o.y, o.z);
-      dir = v3(d.x, d.y, d.z);
       h = pb.hit[q];
       if (depthLevel == 0) {
         // camera rays (k_raygen): throughput 1, depth 0, unbent, vacuum, zero radiance so far;
@@ -1238,13 +1284,20 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       ignoreVL = (meta >> 8) & 1;
       unbent = (meta >> 9) & 1;
       medium = (meta >> 10) & 0xFFFF;  // LightPath::lastMedium as a medium-table index
-      s = path / bi.numPixels;
+      s = fastdiv(path, bi.divPixels);
       const int i = path - s * bi.numPixels;
       batch_pixel(rp, bi, i, px, py);
       pixelId = py * rp.width + px;
-      rec = fv.pixelSets[pixelId] * rp.spp + s;
-      wo = -dir;
       isHit = __float_as_int(h.w) >= 0;
+    }
+    // the ray's direction, origin and sample record are read where they are used: a miss
+    // reads the direction only for an emitting environment light whose Le depends on it, and
+    // neither the origin nor the sample record unless it looks up the backplate (a hit issues
+    // these loads beside its shading record's, off its dependent chain)
+    if (active && (isHit || sv.numEnvDir > 0)) {
+      const float4 d = pb.qDir[cur][q];
+      dir = v3(d.x, d.y, d.z);
+      wo = -dir;
     }
     SPROF_MARK(0);  // queue record, pixel and sample record
     if (active && !isHit) {
@@ -1253,6 +1306,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
         // environment shading (pathtraceintegrator.cpp:79-92): the backplate for a straight
         // camera ray, looked up at the sample's image-plane position (state.pixel)
         if (fv.backplateTexels && unbent) {
+          rec = fv.pixelSets[pixelId] * rp.spp + s;
           const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
           const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
           const GpuImage& bp = fv.backplate;
@@ -1283,6 +1337,9 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       const int gid = __float_as_int(h.w);
       const float4* tsr = (const float4*)(sv.triShade + gid);
       const float4 r0 = tsr[0];
+      const float4 o = pb.qOrg[cur][q];
+      org = v3(o.x, o.y, o.z);
+      rec = fv.pixelSets[pixelId] * rp.spp + s;
       g = __float_as_int(r0.w);  // geometry id rides in the shading record
       const GpuGeomRec& gr = sv.geomRecs[g];
       const int mat = gr.g.material;
@@ -1484,7 +1541,7 @@ __device__ float4* g_dbgOut = nullptr;
 __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, PathBuffers pb, BatchInfo bi,
                                                             float* __restrict__ fbFloat, uint8_t* __restrict__ fbRGB8,
                                                             int rgb8Stride, float4* __restrict__ accu, int accumulate) {
-  const GpuRenderParams& rp = *fv.rp;
+  const YRT_CONST GpuRenderParams& rp = const_ref(fv.rp);
   const size_t frameStride = (size_t)rp.width * rp.height;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < bi.numPixels; i += gridDim.x * blockDim.x) {
     int x, y, f;

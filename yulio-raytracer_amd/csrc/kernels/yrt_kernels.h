@@ -38,6 +38,7 @@ struct SceneView {
   int numLights, numEnvLights, numNodes, numTris;
   int numDirectLights;  // k_shade's direct-light loop and the per-path shadow slots
   int numEnvZero;       // environment lights left out of envLights: radiance exactly 0 (scene_gpu.cpp)
+  int numEnvDir;        // envLights whose Le depends on the direction (HDRI, distant; not ambient)
 };
 
 // Trace grid: 16384 blocks (swept with 128-lane blocks; with 64-lane blocks 32768 is -0.5 %),
@@ -117,6 +118,7 @@ struct BatchInfo {
   int numPixels;       // pixels in the batch (multiple of 256, may overhang the image)
   int tileStride;      // shard: image tile = tileOffset + localTile * tileStride
   int tileOffset;
+  FastDiv divPixels;   // fastdiv_make(numPixels): path id -> (sample, batch pixel)
 };
 
 // Kernel launchers (kernels/pathtrace.hip)
