@@ -1072,7 +1072,8 @@ __device__ __forceinline__ void img_get(const SceneView& sv, int image, int x, i
 }
 
 // HDRILight::Le (lights/hdrilight.cpp:43-71)
-__device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
+template <class LT>  // GpuLight, or a YRT_CONST one (scalar loads)
+__device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const LT& lt, V3 wo) {
   const A3 w2l = ldA3(lt.w2l);
   const V3 wi = xfmVector(w2l, -wo);
   const float theta = yrt_acosf(clampf(wi.y, -1.0f, 1.0f));
@@ -1110,8 +1111,8 @@ __device__ __forceinline__ V3 hdri_Le(const SceneView& sv, const GpuLight& lt, V
 constexpr unsigned kAllLights = 0x7Fu;
 template <unsigned MM>
 constexpr unsigned lights_of() { return (MM >> 16) & kAllLights; }
-template <unsigned LM>
-__device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3 wo) {
+template <unsigned LM, class LT>
+__device__ __forceinline__ V3 env_Le(const SceneView& sv, const LT& lt, V3 wo) {
   if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) return v3(lt.L[0], lt.L[1], lt.L[2]);
   if ((LM & (1u << LIGHT_DISTANT)) && lt.type == LIGHT_DISTANT)  // DistantLight::Le (distantlight.h:38-41)
     return dot(-wo, ld3(lt.e1)) >= lt.bsphere[1] ? v3(lt.L[0], lt.L[1], lt.L[2]) : v3s(0.f);
@@ -1120,8 +1121,8 @@ __device__ __forceinline__ V3 env_Le(const SceneView& sv, const GpuLight& lt, V3
 }
 
 // Light::sample for a non-precomputed light; returns L, sets wi/pdf.
-template <unsigned LM>
-__device__ __forceinline__ V3 light_sample(const GpuLight& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
+template <unsigned LM, class LT>
+__device__ __forceinline__ V3 light_sample(const LT& lt, const DG& dg, float sx, float sy, V3& wi, float& pdf) {
   if ((LM & (1u << LIGHT_AMBIENT)) && lt.type == LIGHT_AMBIENT) {
     // lights/ambientlight.h:52-65 (the bsphere tMax is overwritten by the integrator)
     wi = cosine_hemi_dg(sx, sy, dg, pdf);
@@ -1319,7 +1320,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
         } else if (!ignoreVL) {
           for (int j = 0; j < sv.numEnvLights; ++j) {
             if (!haveL) { const float4 l4 = pb.pathL[path]; L = v3(l4.x, l4.y, l4.z); haveL = true; }
-            L = L + thr * env_Le<lights_of<MM>()>(sv, sv.lights[sv.envLights[j]], wo);
+            L = L + thr * env_Le<lights_of<MM>()>(sv, const_ref(sv.lights + const_ref(sv.envLights + j)), wo);
           }
           // the zero environment lights' throughput * 0: a no-op unless the throughput is not
           // finite, where the reference's add makes the radiance NaN
@@ -1439,11 +1440,11 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); its
     // contribution is added to pathL[path] after the emission above (reference order)
     for (int k = 0; k < numDirect; ++k) {
-      const int li = sv.directLights[k];
+      const int li = const_ref(sv.directLights + k);
       bool pred = false;
       V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
       float tnear = 0.f, tfar = 0.f;
-      const GpuLight& lt = sv.lights[li];
+      const YRT_CONST GpuLight& lt = const_ref(sv.lights + li);  // scalar loads
       const bool lit = active && isHit && useDirect && (lt.illumMask & dg.illumMask) != 0;
       V3 Ls = v3s(0.f);
       float pdf = 0.f;
