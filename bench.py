@@ -44,7 +44,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--size", type=int, default=2048)
     p.add_argument("--spp", type=int, default=64)
-    p.add_argument("--cpu-rows", type=int, default=112, help="rows of the centred CPU-baseline sample")
+    p.add_argument("--cpu-tile-stride", type=int, default=18,
+                   help="CPU-baseline sample: the 16x16 tiles t %% N == 0 of the frame (0: a centred band of --cpu-rows)")
+    p.add_argument("--cpu-rows", type=int, default=112, help="rows of the centred CPU-baseline band (--cpu-tile-stride 0)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--capture", type=int, default=4096,
                    help="rays per depth sampled for visit counts (0: no capture frame, e.g. PMC passes)")
@@ -467,8 +469,10 @@ def single_gpu_cube(args, local, stride):
 
 
 def cpu_baseline(ses, a):
-    """The oracle (CPU restatement of the reference path) on a bounded, centred band of the
-    same frame (a.cpu_rows rows x full width, same spp/depth/scene/camera), on every logical
+    """The oracle (CPU restatement of the reference path) on a bounded sample of the same frame
+    (same spp/depth/scene/camera): by default every a.cpu_tile_stride-th 16x16 tile (t % N == 0,
+    the multi-GPU tile split's shard 0), spread over the whole frame so its rays per sample are
+    the frame's; or a centred band of a.cpu_rows rows (--cpu-tile-stride 0). On every logical
     core this process can use (the reference default numThreads=0 -> all cores,
     common/sys/taskscheduler.cpp:105): one worker thread per CPU of the affinity
     mask, capped at the cgroup CPU quota when one is set (the GPU box grants 16 CPUs of a
@@ -480,15 +484,20 @@ def cpu_baseline(ses, a):
     threads = info["affinity"]
     if info["cgroup_cpu_quota"]:
         threads = max(1, min(threads, int(info["cgroup_cpu_quota"])))
-    y0 = (a.size - a.cpu_rows) // 2
     t = time.perf_counter()
-    _, st = oracle.render(blob, a.size, a.size, ses.info()["gamma"], rect=(0, y0, a.size, y0 + a.cpu_rows),
-                          threads=threads)
+    if a.cpu_tile_stride > 0:
+        _, st = oracle.render_shard(blob, a.size, a.size, ses.info()["gamma"], 0, a.cpu_tile_stride, threads=threads)
+        what = f"16x16 tiles t % {a.cpu_tile_stride} == 0 of the {a.size}^2 frame"
+    else:
+        y0 = (a.size - a.cpu_rows) // 2
+        _, st = oracle.render(blob, a.size, a.size, ses.info()["gamma"], rect=(0, y0, a.size, y0 + a.cpu_rows),
+                              threads=threads)
+        what = f"rows [{y0},{y0 + a.cpu_rows}) x {a.size} px of the frame"
     dt = time.perf_counter() - t
     rays = st["raysClosest"] + st["raysShadow"]
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"rows [{y0},{y0 + a.cpu_rows}) x {a.size} px at {a.spp} spp of the same frame "
-                      f"({rays:.0f} rays in {dt:.1f} s)",
+            "sample": f"{what} at {a.spp} spp ({st['samples']:.0f} samples, {rays:.0f} rays, "
+                      f"{rays / max(st['samples'], 1):.2f} rays per sample, in {dt:.1f} s)",
             "samples_per_s": round(st["samples"] / dt, 1), "nproc": info["nproc"], "cpu_model": info["model"],
             "cgroup_cpu_quota": info["cgroup_cpu_quota"], "affinity_cpus": info["affinity"]}
 

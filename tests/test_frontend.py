@@ -106,14 +106,16 @@ def test_startrt_writes_cubemap_jpeg(tmp_path):
 
 @pytest.mark.gpu
 def test_stoprt_cancels_a_running_render(tmp_path):
-    """StopRT during a long StartRT (default ParamsRT: 1536^2 faces, 256 spp): a second
-    StartRT is refused with RenderingIsInProgress, the stop flag ends the render at the next
-    wavefront batch, the state becomes Stopped and, keepResults = false, no image is left
-    (renderer.cpp:724-731, 1606-1641)."""
+    """StopRT during a long StartRT (default ParamsRT but 4096 spp: 1536^2 faces; the cubemap
+    at the default 256 spp — a camera outside the open box, mostly sky — now renders in about
+    a second, within the sleep below): a second StartRT is refused with RenderingIsInProgress,
+    the stop flag ends the render at the next wavefront batch, the state becomes Stopped and,
+    keepResults = false, no image is left (renderer.cpp:724-731, 1606-1641)."""
     import time
     for f in ("cornell_box.ecs", "cornell_box.obj", "cornell_box.mtl"):
         shutil.copy(SCENES / f, tmp_path / f)
     p = yrt.InitParamsRT()
+    p.spp = 4096
     assert yrt.StartRT(tmp_path / "cornell_box.ecs", p)
     assert not yrt.StartRT(tmp_path / "cornell_box.ecs", p)
     assert yrt.GetLastErrorRT() == 1  # RenderingIsInProgress
