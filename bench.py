@@ -495,10 +495,18 @@ def cpu_baseline(ses, a):
         what = f"rows [{y0},{y0 + a.cpu_rows}) x {a.size} px of the frame"
     dt = time.perf_counter() - t
     rays = st["raysClosest"] + st["raysShadow"]
+    # the oracle's sample count is the whole frame's; the sample's own is its pixels x spp
+    tx, ty = (a.size + 15) // 16, (a.size + 15) // 16
+    if a.cpu_tile_stride > 0:
+        px = sum(min(16, a.size - 16 * (t % tx)) * min(16, a.size - 16 * (t // tx))
+                 for t in range(0, tx * ty, a.cpu_tile_stride))
+    else:
+        px = a.cpu_rows * a.size
+    samples = float(px) * a.spp
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{what} at {a.spp} spp ({st['samples']:.0f} samples, {rays:.0f} rays, "
-                      f"{rays / max(st['samples'], 1):.2f} rays per sample, in {dt:.1f} s)",
-            "samples_per_s": round(st["samples"] / dt, 1), "nproc": info["nproc"], "cpu_model": info["model"],
+            "sample": f"{what} at {a.spp} spp ({px} px, {samples:.0f} samples, {rays:.0f} rays, "
+                      f"{rays / max(samples, 1):.2f} rays per sample, in {dt:.1f} s)",
+            "samples_per_s": round(samples / dt, 1), "nproc": info["nproc"], "cpu_model": info["model"],
             "cgroup_cpu_quota": info["cgroup_cpu_quota"], "affinity_cpus": info["affinity"]}
 
 if __name__ == "__main__":

@@ -173,6 +173,20 @@ def test_c4_stereo_face_parity(gpu_device, face):
     parity(img, ref, 0.995)
 
 
+@pytest.mark.parametrize("which", ["C2 200x120", "C4 face 0 72^2", "C4 face 5 72^2"])
+def test_partial_tile_sizes_parity(gpu_device, which):
+    """Images whose sides are not multiples of the 16-pixel tile (the last tile row/column
+    overhangs the image): the batch pixel mapping (multiply-high tile division, overhang lanes
+    left out of the queues) and the stereo camera's host-side terms on a non-square tile grid."""
+    if which.startswith("C2"):
+        img, ref, st = _render_pair(gpu_device, c2_args(200, 4) + ["-size", "200", "120"])
+        assert img.shape[:2] == (120, 200) and st["samples"] == 200 * 120 * 4
+        parity(img, ref, 0.999)
+    else:
+        img, ref, _ = _render_pair(gpu_device, c4_args(72, 4), face=int(which.split()[2]))
+        parity(img, ref, 0.995)
+
+
 def _hdri_scene(L=(2.0, 1.5, 1.2)):
     """models/test_stereo.xml with the HDRI radiance its authors left commented out
     (test_stereo.xml:100 `<L>2.0 1.5 1.2</L>`) switched on; texture paths made absolute."""

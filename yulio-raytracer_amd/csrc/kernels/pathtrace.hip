@@ -306,42 +306,43 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
   const YRT_CONST GpuRenderParams& rp = const_ref(fv.rp);
   const int P = bi.numPixels * rp.spp;
   for (int base = blockIdx.x * blockDim.x; base < P; base += gridDim.x * blockDim.x) {
+    // P is a multiple of 256 and base of the block size: every lane has p < P
     const int p = base + threadIdx.x;
-    bool valid = false;
-    V3 org = v3s(0.f), dir = v3s(0.f);
-    float rtime = 0.f;
-    if (p < P) {  // P and numPixels are multiples of 256: whole waves are in or out
-      // the block's paths share the sample index, the tile and the frame (numPixels is a
-      // multiple of 256): computed once from the block base, on the scalar unit
-      const int s = fastdiv(base, bi.divPixels);
-      int x0 = 0, y0 = 0, f = 0;
-      const bool tileOk = batch_tile(rp, bi, (base - s * bi.numPixels) >> 8, x0, y0, f);
-      const int x = x0 + (p & 15), y = y0 + ((p >> 4) & 15);
-      valid = tileOk && x < rp.width && y < rp.height;
-      const YRT_CONST GpuCamera& cam = const_ref(fv.cam + f);  // scalar loads
-      if (valid) {
-        const int set = fv.pixelSets[(size_t)y * rp.width + x];
-        const int rec = set * rp.spp + s;
-        const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
-        const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
-        camera_ray(cam, fx, fy, org, dir, samp(fv, 2, rec), samp(fv, 3, rec));  // sample.getLens()
-        if (pb.qTime[0]) rtime = samp(fv, 4, rec);  // primary.time = sample.getTime() (:159)
-      }
-      // loop head of Li: depth < maxDepth and max(throughput)=1 >= minContribution
-      valid = valid && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
-    }
-    bool got;
+    // the block's paths share the sample index, the tile and the frame (numPixels is a
+    // multiple of 256): computed once from the block base, on the scalar unit
+    const int s = fastdiv(base, bi.divPixels);
+    int x0 = 0, y0 = 0, f = 0;
+    const bool tileOk = batch_tile(rp, bi, (base - s * bi.numPixels) >> 8, x0, y0, f);
+    const int x = x0 + (p & 15), y = y0 + ((p >> 4) & 15);
+    // a pixel of the image, and the loop head of Li: depth < maxDepth and
+    // max(throughput) = 1 >= minContribution
+    const bool valid = tileOk && x < rp.width && y < rp.height && rp.maxDepth > 0 && !(1.0f < rp.minContribution);
+    // queue slots first: the append's atomic is issued before the camera ray is computed and
+    // its result is read at the stores, so its round trip overlaps the sample loads and the
+    // camera arithmetic (the leader lane's counter value is broadcast after)
     const int seg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
-    const unsigned q = seg * pb.segCap + wave_append(pb.counters + qcounter_index(0, 0, seg), valid, got);
-    // the camera ray's throughput (1, 1, 1), its meta word (depth 0, unbent) and its zero
-    // radiance are implicit at depth 0: k_shade starts from them and writes pathL of every
-    // queued path, so only the paths that are not queued get their zero radiance here
-    if (got) {
+    const unsigned long long vmask = ballot(valid);
+    const int leader = vmask ? __ffsll((long long)vmask) - 1 : 0;
+    unsigned qbase = 0;
+    if (vmask && lane_id() == leader) qbase = atomicAdd(pb.counters + qcounter_index(0, 0, seg), (unsigned)__popcll(vmask));
+    if (valid) {
+      const YRT_CONST GpuCamera& cam = const_ref(fv.cam + f);  // scalar loads
+      const int set = fv.pixelSets[(size_t)y * rp.width + x];
+      const int rec = set * rp.spp + s;
+      const float fx = (float(x) + samp(fv, 0, rec)) * rp.rcpWidth;
+      const float fy = (float(y) + samp(fv, 1, rec)) * rp.rcpHeight;
+      V3 org, dir;
+      camera_ray(cam, fx, fy, org, dir, samp(fv, 2, rec), samp(fv, 3, rec));  // sample.getLens()
+      // the camera ray's throughput (1, 1, 1), its meta word (depth 0, unbent) and its zero
+      // radiance are implicit at depth 0: k_shade starts from them and writes pathL of every
+      // queued path, so only the paths that are not queued get their zero radiance here
+      const unsigned q = seg * pb.segCap + (unsigned)__builtin_amdgcn_readlane((int)qbase, leader) +
+                         (unsigned)__popcll(vmask & ((1ull << lane_id()) - 1ull));
       pb.qPath[0][q] = p;
       pb.qOrg[0][q] = make_float4(org.x, org.y, org.z, 0.f);
       pb.qDir[0][q] = make_float4(dir.x, dir.y, dir.z, __int_as_float(0x7f800000));
-      if (pb.qTime[0]) pb.qTime[0][q] = rtime;
-    } else if (p < P) {
+      if (pb.qTime[0]) pb.qTime[0][q] = samp(fv, 4, rec);  // primary.time = sample.getTime() (:159)
+    } else {
       pb.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
