@@ -164,7 +164,7 @@ def main():
     rays, closest, shadow = tot.tolist()
     elapsed = tmax.item()
 
-    stereo = stereo_cubemap(a, dev, rank, world, backend, gather, local) if a.stereo_frames > 0 else None
+    stereo = stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used) if a.stereo_frames > 0 else None
 
     if rank == 0:
         # dominant trace kernel: what binds it. The BVH and the
@@ -364,7 +364,7 @@ def cpu_info():
             "cgroup_cpu_quota": quota}
 
 
-def stereo_cubemap(a, dev, rank, world, backend, gather, local):
+def stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used):
     """BASELINE.json configs[3]: the test_stereo stereo cubemap (12 faces x 1536^2, 256 spp,
     depth 10, test_stereo_view.ecs) as one job per cubemap (yrtRenderFrames): the 110,592
     16x16 tiles of the 12 faces dealt round-robin over the ranks and gathered on
@@ -421,7 +421,7 @@ def stereo_cubemap(a, dev, rank, world, backend, gather, local):
     c4 = (W, a.stereo_spp) == (1536, 256)
     out = {"metric": f"Mrays/s (test_stereo stereo cubemap 12x{W}^2 {a.stereo_spp}spp, closest+shadow queries)",
            "workload": "C4" if c4 else "C4-reduced",
-           "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": world,
+           "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": gpus_used, "ranks": world,
            "scaling": "strong", "ms_per_cubemap": round(dt / a.stereo_frames * 1e3, 1),
            "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
            "parallelism": f"cube-tiles-roundrobin{world}", "gather": "C++ RCCL" if cxx else "torch reduce",

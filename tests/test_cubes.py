@@ -285,5 +285,6 @@ def test_bench_two_ranks_cubemap_gather_check(tmp_path):
     assert line["ranks"] == 2 and line["n_gpus"] == 1  # two ranks, one physical GPU
     sc = line["stereo_cubemap"]
     assert sc is not None and sc["scaling"] == "strong" and sc["value"] > 0
+    assert sc["ranks"] == 2 and sc["n_gpus"] == 1
     assert sc["gather_check"] == "bit_exact", sc
     assert sc["single_gpu_ms_per_cubemap"] > 0
