@@ -689,10 +689,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             float t, U, V, absDen;
             const bool g = tri_test_g(tt[k], r, t, U, V, absDen);
             const int gid = __float_as_int(tt[k].v0[3]);
-            // tri_test_t's range test against the current closest hit; ties (t == best.t)
-            // fail it and are re-tested against the ray's tfar: the smaller id wins
-            bool ok = g & (t > r.tnear) & (t < best.t + 0.0f);
-            if (!ok && best.tri >= 0 && t == best.t && gid < best.tri) ok = g & (t > r.tnear) & (t < r.tfar);
+            // range test against the current closest hit; on a tie (t == best.t) the smaller
+            // triangle id wins
+            // a tie with an accepted hit (best.tri >= 0, so best.t < tfar) passes the range test
+            // by itself: one predicate instead of a re-test against tfar (C3 -0.35 %, C5 -0.3 %)
+            const bool tie = (t == best.t) & (best.tri >= 0) & (gid < best.tri);
+            const bool ok = g & (t > r.tnear) & ((t < best.t + 0.0f) | tie);
             if (ok & (k < lTake)) {
               best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
             }
