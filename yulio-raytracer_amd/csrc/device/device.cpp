@@ -174,7 +174,10 @@ class Device {
   int hipDevice = 0;                         // ctx[0]'s
   hipStream_t stream = nullptr;              // ctx[0]'s
   uint32_t frameSeed = 0x2545F491u;
-  int64_t capacity = 64ll << 20;  // paths per batch: C3 +4 % over 16 M (fewer launch tails), ~10 GB
+#ifndef YRT_DEFAULT_CAPACITY_M
+#define YRT_DEFAULT_CAPACITY_M 64
+#endif
+  int64_t capacity = (int64_t)YRT_DEFAULT_CAPACITY_M << 20;  // paths per batch: C3 +4 % over 16 M (fewer launch tails), ~10 GB
   // process-level shard (yrtSetTileShard / yrtSetShardComm): this process renders tiles
   // t = shardIndex (mod shardCount), dealt over its own devices
   int shardIndex = 0, shardCount = 1;
