@@ -34,6 +34,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md §HBM
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md §L2 (per XCD, 32 MiB aggregate): ≈34.5 TB/s
 NODE_BYTES = 128  # GpuNode (4-wide); triangle record bytes from the scene (GpuTri, 48 or 64)
 
 
@@ -55,10 +56,10 @@ def parse():
     p.add_argument("--stereo-spp", type=int, default=256, help="cube spp (C4: 256; smaller for tests)")
     p.add_argument("--stereo-frames", type=int, default=None,
                    help="C4 stereo cubemaps (12 x 1536^2 x 256spp, one job, tiles dealt over the ranks) timed "
-                        "after the main loop and reported under 'stereo_cubemap'. Default: 1 at N>1 (the "
-                        "BASELINE 1/2/4/8-GPU cubemap, gather checked against a one-GPU render), 0 at N=1 so "
-                        "a rocprof summary of the default command averages only the C3 launches of the "
-                        "roofline kernel")
+                        "after the main loop and reported under 'stereo_cubemap' (median and min per cubemap). "
+                        "Default: 6 at N>1 (the BASELINE 1/2/4/8-GPU cubemap, gather checked against a one-GPU "
+                        "render), 0 at N=1 so a rocprof summary of the default command averages only the C3 "
+                        "launches of the roofline kernel")
     return p.parse_args()
 
 
@@ -76,7 +77,7 @@ def main():
         local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if a.stereo_frames is None:
-        a.stereo_frames = 1 if world > 1 else 0
+        a.stereo_frames = 6 if world > 1 else 0
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -181,6 +182,7 @@ def main():
         avg_ms = ms / max(nl, 1)
         kname = "k_trace<false>" if dom == "closest" else "k_trace<true>"
         alg = nr * per_kind[dom]["bytes_per_ray"] / max(nl, 1) if per_kind else None
+        alg_gbs = alg / (avg_ms * 1e-3) / 1e9 if alg and avg_ms > 0 else None
         pmc, pmc_note = load_pmc(a, sinfo, world)
         kp = (pmc or {}).get("kernels", {}).get(kname, {})
         traffic = kp.get("hbm_bytes_per_dispatch")
@@ -198,13 +200,23 @@ def main():
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
                         "bytes_per_launch": round(traffic) if traffic else None},
                 "algorithmic_bytes_per_launch": round(alg) if alg else None,
+                # north_star's "fraction of HBM roofline", read directly: the SURVEY 8(d) bytes per
+                # launch over the launch time, against HBM and against the L2 (where they are served)
+                "algorithmic_gbs": round(alg_gbs, 1) if alg_gbs else None,
+                "algorithmic_hbm_frac": round(alg_gbs / HBM_PEAK_GBS, 4) if alg_gbs else None,
+                "l2_frac": round(alg_gbs / L2_PEAK_GBS, 4) if alg_gbs else None,
+                "l2_peak_gbs": L2_PEAK_GBS,
                 "algorithmic_note": "SURVEY 8(d) bytes (ray+hit+N_node*128+N_tri*48); node/triangle reads are "
-                                    "L2/MALL hits, so this is not an HBM rate",
+                                    "L2/MALL hits (counter HBM traffic is 'hbm'), so algorithmic_hbm_frac can exceed "
+                                    "1; l2_frac is the same bytes against the L2 peak",
                 "pmc_source": pmc_note,
                 "visits": per_kind,
                 "kernel_ms_per_step": {"trace_closest": acc["msClosest"] / a.steps,
                                        "trace_shadow": acc["msShadow"] / a.steps,
-                                       "shade": acc["msShade"] / a.steps}}
+                                       "shade": acc["msShade"] / a.steps,
+                                       "note": "HIP-event time per kernel kind, summed per step; the two "
+                                               "wavefront lanes' kernels overlap, so these are not additive "
+                                               "(their sum exceeds ms_per_step)"}}
         cpu = None
         if not a.no_cpu_baseline:
             cpu = cpu_baseline(ses, a)
@@ -403,26 +415,32 @@ def stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used):
         dist.barrier()
     torch.cuda.synchronize()
     rays = 0.0
+    per = []  # this rank's time per cubemap (the C++ gather ends each one on rank 0)
     t0 = time.perf_counter()
     for _ in range(a.stereo_frames):
+        t1 = time.perf_counter()
         rays += one_cube()
+        per.append(time.perf_counter() - t1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     red = "cuda" if backend == "nccl" else "cpu"
     tot = torch.tensor([rays], dtype=torch.float64, device=red)
-    tm = torch.tensor([dt], dtype=torch.float64, device=red)
+    tm = torch.tensor([dt] + per, dtype=torch.float64, device=red)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-    dt = tm.item()
+    dt = tm[0].item()
+    per = sorted(tm[1:].tolist())  # per cubemap, max over ranks
     samples = 12.0 * W * H * a.stereo_spp * a.stereo_frames
     c4 = (W, a.stereo_spp) == (1536, 256)
     out = {"metric": f"Mrays/s (test_stereo stereo cubemap 12x{W}^2 {a.stereo_spp}spp, closest+shadow queries)",
            "workload": "C4" if c4 else "C4-reduced",
            "value": round(tot.item() / dt / 1e6, 2), "unit": "Mrays/s", "n_gpus": gpus_used, "ranks": world,
            "scaling": "strong", "ms_per_cubemap": round(dt / a.stereo_frames * 1e3, 1),
+           "ms_per_cubemap_median": round(float(np.median(per)) * 1e3, 1),
+           "ms_per_cubemap_min": round(per[0] * 1e3, 1),
            "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
            "parallelism": f"cube-tiles-roundrobin{world}", "gather": "C++ RCCL" if cxx else "torch reduce",
            "gather_check": None}

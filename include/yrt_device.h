@@ -111,13 +111,14 @@ YRT_API int yrtCommit(YRTDevice dev, YRTHandle h);
 YRT_API int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene,
                            YRTHandle tonemapper, YRTHandle framebuffer, int accumulate);
 /* Several frames of one scene in one wavefront job: frame k seen through cameras[k] into
- * framebuffers[k] (all the same size and format). The result equals numFrames rtRenderFrame
- * calls with the same accumulate flag, bit for bit (the per-tile Random of
+ * framebuffers[k] (all the same size and format). With accumulate = 0 the result equals
+ * numFrames rtRenderFrame calls with accumulate = 0, bit for bit (the per-tile Random of
  * integratorrenderer.cpp:134 and every per-pixel input depend on the frame's own pixel only),
  * but the frames' 16x16 tiles form one sequence (frame-major) that fills the batches and is
  * dealt over shards and GPUs as a whole, with one gather per job. This is the loop of the
  * stereo-cube drivers over the 12 faces of a view (renderer.cpp:543-737, 742-878) when no
- * primitive changes between the faces. */
+ * primitive changes between the faces. accumulate != 0 is accepted for numFrames == 1 only (a
+ * job keeps one sampler iteration and no per-frame accumulation state across calls). */
 YRT_API int yrtRenderFrames(YRTDevice dev, YRTHandle renderer, const YRTHandle* cameras, int numFrames,
                             YRTHandle scene, YRTHandle tonemapper, const YRTHandle* framebuffers, int accumulate);
 YRT_API void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle framebuffer, int bufID);
@@ -158,7 +159,14 @@ typedef struct YRTRenderStats {
   double launchesShadow;
   double nodeVisits;      /* reserved (0): visit counts come from oracle_count_visits */
   double triVisits;
+  double gather;          /* how the frame was gathered: YRT_GATHER_* */
 } YRTRenderStats;
+#define YRT_GATHER_NONE 0           /* one device, no gather */
+#define YRT_GATHER_D2D 1            /* logical shards of one GPU: device-to-device copy */
+#define YRT_GATHER_RCCL_LOCAL 2     /* distinct GPUs of one process: RCCL (ncclCommInitAll) send/recv */
+#define YRT_GATHER_PEER_COPY 3      /* distinct GPUs, RCCL unavailable or timed out: hipMemcpyPeerAsync */
+#define YRT_GATHER_RCCL_PROCESS 4   /* one process per GPU: RCCL communicator (yrtSetShardComm) */
+#define YRT_GATHER_HUB 5            /* several devices of one process: shard hub (yrtSetShardHub) */
 YRT_API int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out);
 /* 1 = bracket every kernel with HIP events (adds sync-free event records). */
 YRT_API int yrtSetKernelTiming(YRTDevice dev, int enable);
@@ -196,12 +204,35 @@ YRT_API int yrtSetTileShard(YRTDevice dev, int index, int count);
  * tile slab to rank 0, whose framebuffer then holds the whole frame. */
 YRT_API int yrtShardCommUniqueId(void* id128);
 /* Every rank of a job calls yrtSetShardComm (collective: RCCL ncclCommInitRank). Before each
- * gather the ranks exchange their render status, so a rank whose render throws makes every
- * rank's yrtRenderFrame fail instead of leaving rank 0 waiting. world = 1 drops the
- * communicator. The gathered slabs carry 4 bytes per pixel for RGB8 framebuffers (16 else).
+ * gather the ranks exchange their render status, so a rank whose render throws (or whose
+ * render call fails on its arguments) makes every rank's yrtRenderFrame fail instead of
+ * leaving rank 0 waiting. Every wait of the gather is bounded (yrtSetGatherTimeout): on expiry
+ * the communicator is aborted (ncclCommAbort) and the call fails with the phase that timed
+ * out; later gathers on it fail at once. world = 1 drops the communicator. The gathered slabs carry 4 bytes per pixel for RGB8 framebuffers (16 else).
  * Only rank 0's framebuffers receive pixels; the other ranks' host framebuffers are left as
  * they were (their part of the frame is already on rank 0). */
 YRT_API int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128);
+/* The same gather between several devices of one process (threads; they may share a GPU):
+ * yrtNewShardHub(world) is the meeting point, and yrtSetShardHub(dev, hub, rank) arms device
+ * `rank` (tile shard rank of world) exactly as yrtSetShardComm would; hub = NULL disarms. The
+ * slabs move by hipMemcpyPeerAsync (device-to-device on one GPU). This runs the process
+ * gather's bookkeeping — status exchange, per-rank tile counts, pack, unpack, the failing-rank
+ * path — on one GPU. A device keeps the hub alive; yrtDeleteShardHub drops the caller's. */
+typedef struct YRTShardHub_* YRTShardHub;
+YRT_API YRTShardHub yrtNewShardHub(int world);
+YRT_API void yrtDeleteShardHub(YRTShardHub hub);
+YRT_API int yrtSetShardHub(YRTDevice dev, YRTShardHub hub, int rank);
+/* Bound, in seconds, of every wait of a gather (status exchange, slab send/recv); default
+ * YRT_GATHER_TIMEOUT_S or 300. The status exchange also waits for the slowest rank's render. */
+YRT_API int yrtSetGatherTimeout(YRTDevice dev, double seconds);
+/* Host-memory forms of the hub's two phases (CPU tests of its deadlines and size checks):
+ * yrtShardHubStatus returns the min of the ranks' flags (or -1), yrtShardHubSlab sends `bytes`
+ * to rank 0 (rank > 0) or receives every peer's recvBytesPerRank bytes into recv in rank
+ * order (rank 0). Errors: -1 and yrtShardHubLastError() (per calling thread). */
+YRT_API int yrtShardHubStatus(YRTShardHub hub, int rank, int flag, double timeoutS);
+YRT_API int yrtShardHubSlab(YRTShardHub hub, int rank, const void* slab, size_t bytes, void* recv,
+                            size_t recvBytesPerRank, double timeoutS);
+YRT_API const char* yrtShardHubLastError(void);
 /* 1 when librccl can be loaded (checked on every rank before the collective comm init). */
 YRT_API int yrtRcclAvailable(void);
 /* HIP devices (logical shards) this device renders on (yrtNewDevice "devices=..."). */

@@ -140,3 +140,60 @@ def test_tangent_arrays_parity(gpu_device):
     img = d.framebuffer_array(fb, 64, 64, "RGB_FLOAT32")
     ref, _ = oracle.render(d.export_frame(r, cam, scene), 64, 64, 1.0)
     parity(img, ref, 0.999)
+
+
+def _sphere_scene(d, dpdt=None):
+    """A Matte sphere under a dome; `dpdt` sets the sphere's motion (sphere.h:38,67)."""
+    from test_cpu_host import yrt_lookat
+    sph = d.rtNewShape("sphere")
+    d.rtSetFloat3(sph, "P", 0.0, 0.0, 0.0)
+    d.rtSetFloat1(sph, "r", 1.0)
+    d.rtSetInt1(sph, "numTheta", 16)
+    d.rtSetInt1(sph, "numPhi", 32)
+    if dpdt is not None:
+        d.rtSetFloat3(sph, "dPdt", *dpdt)
+    d.rtCommit(sph)
+    mat = d.rtNewMaterial("Matte")
+    d.rtSetFloat3(mat, "reflectance", 0.7, 0.5, 0.3)
+    d.rtCommit(mat)
+    amb = d.rtNewLight("ambientlight")
+    d.rtSetFloat3(amb, "L", 1.0, 1.0, 1.0)
+    d.rtCommit(amb)
+    cam = d.rtNewCamera("pinhole")
+    d.rtSetTransform(cam, "local2world", yrt_lookat((0, 0, -4), (0, 0, 0), (0, 1, 0)))
+    d.rtSetFloat1(cam, "angle", 50.0)
+    d.rtSetFloat1(cam, "aspectRatio", 1.0)
+    d.rtCommit(cam)
+    r = d.rtNewRenderer("pathtracer")
+    d.rtSetInt1(r, "maxDepth", 2)
+    d.rtSetInt1(r, "sampler.spp", 8)
+    d.rtCommit(r)
+    tm = d.rtNewToneMapper("default")
+    d.rtCommit(tm)
+    fb = d.rtNewFrameBuffer("RGB_FLOAT32", 48, 48)
+    return sph, mat, amb, cam, r, tm, fb
+
+
+@pytest.mark.gpu
+def test_recommit_with_changed_motion_rebuilds(gpu_device):
+    """A scene re-committed after its sphere gained a dPdt (same vertices at t = 0) must render
+    the moving sphere: the faceCamera refit re-uploads positions and normals only, so the commit
+    rebuilds instead (the old compare saw 'same geometry' and kept the static scene)."""
+    d = gpu_device
+    sph, mat, amb, cam, r, tm, fb = _sphere_scene(d)
+    scene = d.rtNewScene("default")
+    d.rtSetPrimitive(scene, 0, d.rtNewShapePrimitive(sph, mat))
+    d.rtSetPrimitive(scene, 1, d.rtNewLightPrimitive(amb))
+    d.rtCommit(scene)
+    d.rtRenderFrame(r, cam, scene, tm, fb, 0)
+    static = d.framebuffer_array(fb, 48, 48, "RGB_FLOAT32").copy()
+    d.rtSetFloat3(sph, "dPdt", 0.6, 0.0, 0.0)
+    d.rtCommit(sph)
+    d.rtSetPrimitive(scene, 0, d.rtNewShapePrimitive(sph, mat))
+    d.rtCommit(scene)
+    assert d.scene_refits(scene) == 0  # rebuilt, not refit
+    d.rtRenderFrame(r, cam, scene, tm, fb, 0)
+    moving = d.framebuffer_array(fb, 48, 48, "RGB_FLOAT32")
+    ref, _ = oracle.render(d.export_frame(r, cam, scene), 48, 48, 1.0)
+    assert not np.array_equal(moving, static)
+    parity(moving, ref, 0.999)

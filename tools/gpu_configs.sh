@@ -2,7 +2,7 @@
 # GPU-box, round-3 evidence part B: the C4 cubemap strong-scaling prediction (one GPU, every
 # rank's share), the C5 cube job render-only at 1024 spp, and every BASELINE config with the CPU
 # restatement beside it.
-# usage: tools/gpu_r3_finalB.sh <tag>
+# usage: tools/gpu_configs.sh <tag>
 export TMPDIR=/tmp
 TAG=${1:-r3f}
 R=$GRAFT_REPO_ROOT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box: PMC passes of the C3 bench workload (-> pmc.json), then the default bench line reading
 # it, and the same command under rocprofv3 kernel stats (tree already through the GPU suite).
-# usage: tools/gpu_r3_finalP.sh <tag>
+# usage: tools/gpu_evidence_c3.sh <tag>
 export TMPDIR=/tmp
 TAG=${1:-r3p}
 R=$GRAFT_REPO_ROOT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box: GPU suite and smoke() on the working tree, the default bench line, and the N=2
 # gloo rehearsal of bench.py (two ranks on this one GPU).
-# usage: tools/gpu_r3_suite.sh <tag>
+# usage: tools/gpu_suite.sh <tag>
 export TMPDIR=/tmp
 TAG=${1:-suite}
 R=$GRAFT_REPO_ROOT

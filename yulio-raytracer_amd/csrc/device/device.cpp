@@ -23,6 +23,7 @@
 #include "image_io.h"
 #include "objects.h"
 #include "scene_gpu.h"
+#include "gather.h"
 #include "rccl_comm.h"
 #include "sampler.h"
 
@@ -181,11 +182,17 @@ class Device {
   // process-level shard (yrtSetTileShard / yrtSetShardComm): this process renders tiles
   // t = shardIndex (mod shardCount), dealt over its own devices
   int shardIndex = 0, shardCount = 1;
-  ncclComm_t procComm = nullptr;     // process-level gather to rank 0 (yrtSetShardComm)
-  int commRank = 0, commWorld = 1;   // procComm's rank / size: the only shard it gathers
-  DevBuf dCommFlag;                  // per-frame render status exchanged before the gather
+  // process-level gather to rank 0 (gather.h): RCCL (yrtSetShardComm) or an in-process hub
+  // of several Device objects (yrtSetShardHub)
+  std::unique_ptr<GatherTransport> proc;
+  int commRank = 0, commWorld = 1;   // proc's rank / size: the only shard it gathers
+  double gatherTimeout = default_gather_timeout();  // bound of every gather wait (yrtSetGatherTimeout)
   ncclComm_t localComm = nullptr;    // the ctx devices' gather (distinct devices only): rank 0's
   std::vector<ncclComm_t> localComms;  // one per ctx device (ncclCommInitAll)
+  // ncclCommInitAll failed (or a gather over it timed out): distinct devices gather with
+  // hipMemcpyPeerAsync instead, reported as YRT_GATHER_PEER_COPY in the render stats
+  bool localRcclOff = getenv("YRT_NO_LOCAL_RCCL") != nullptr;
+  std::string localRcclWhy;
   bool refitCommits = true;  // SceneObj::commit refits faceCamera-only changes (yrtSetRefitCommits)
   bool kernelTiming = false;
   YRTRenderStats stats{};
@@ -204,14 +211,14 @@ class Device {
   DevBuf dbgPixelBuf;   // yrtDebugPixelSamples capture (a debugging aid), armed on this device
   int dbgPixelCap = 0;
   ~Device() {
-    if (dbgPixelBuf.p) (void)debug_pixel_capture(-1, -1, nullptr);  // no kernel may write it once freed
+    if (dbgPixelBuf.p) (void)debug_pixel_capture(-1, -1, nullptr, 0);  // no kernel may write it once freed
     for (auto* h : handles) delete h;
     handles.clear();
     try {
       for (auto c : localComms) rccl().CommDestroy(c);
-      if (procComm) rccl().CommDestroy(procComm);
     } catch (...) {
     }
+    proc.reset();
   }
 
   YRTHandle wrap(std::shared_ptr<Object> o) {
@@ -254,8 +261,21 @@ class Device {
               const std::vector<FrameBufferObj*>& F, int accumulate);
   void render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vector<CameraObj*>& C, ToneMapperObj& T,
                     int W, int H, int index, int count, int accumulate, bool reportProgress);
-  void gather_local(const SlabLayout& base, int numTiles);
+  int gather_local(const SlabLayout& base, int numTiles);
   void gather_process(const SlabLayout& base, int numTiles, bool localOk);
+  // a process gather is armed: every render of this device joins the ranks' status exchange
+  bool proc_gather_armed() const {
+    return proc && shardCount > 1 && shardIndex == commRank && shardCount == commWorld;
+  }
+  // A render call that fails before reaching render() (bad handles, host-only device) still
+  // joins the status exchange with flag 0, so the peers fail instead of waiting for it.
+  void fail_proc_gather() {
+    if (!proc_gather_armed() || proc->aborted()) return;
+    try {
+      (void)proc->exchange_status(0, hipDevice, stream, gatherTimeout);
+    } catch (...) {
+    }
+  }
   void intersect(SceneObj& S, const float* org4, const float* dir4, uint32_t n, float* hit4, int32_t* occ,
                  hipStream_t st);
 };
@@ -271,7 +291,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
   // A process-level gather (yrtSetShardComm) is collective: every rank must reach it, so any
   // failure of this rank's part (arguments, scene, kernels) is reported to the peers through
   // the status exchange at its start instead of being thrown past it.
-  const bool procGather = !R.debug && procComm && shardCount > 1 && shardIndex == commRank && shardCount == commWorld;
+  const bool procGather = !R.debug && proc_gather_armed();
   const int nf = (int)F.size();
   const int W = nf ? F[0]->width : 0, H = nf ? F[0]->height : 0;
   const int tilesPerFrame = ((W + 15) / 16) * ((H + 15) / 16);
@@ -282,6 +302,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
   // the debug renderer is a one-pass traversal KAT: the primary device renders every tile
   const int nr = R.debug ? 1 : N;
   std::string localErr;
+  int gatherPath = YRT_GATHER_NONE;
   try {
     if (!S.gpu) throw std::runtime_error("scene not committed");
     if (S.gpu->device != hipDevice) throw std::runtime_error("scene committed on another HIP device");
@@ -323,13 +344,16 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
       for (auto& t : th) t.join();
       for (auto& e : errs)
         if (!e.empty()) throw std::runtime_error(e);
-      gather_local(base, numTiles);
+      gatherPath = gather_local(base, numTiles);
     }
   } catch (const std::exception& e) {
     if (!procGather) throw;
     localErr = e.what();
   }
-  if (procGather) gather_process(base, numTiles, localErr.empty());
+  if (procGather) {
+    gather_process(base, numTiles, localErr.empty());
+    gatherPath = proc->kind()[0] == 'r' ? YRT_GATHER_RCCL_PROCESS : YRT_GATHER_HUB;
+  }
   if (!localErr.empty()) throw std::runtime_error(localErr);
   R.iteration++;
   for (int k = 0; k < nr; ++k) {
@@ -377,6 +401,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     }
   }
   stats.samples = ctx[0]->stats.samples;
+  stats.gather = gatherPath;
   stats.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   status(R, 2, 1.f);
 }
@@ -725,8 +750,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
 
 // The ctx devices' shards onto ctx[0]: every peer packs its tiles into a slab, the slabs go to
 // the first device (RCCL grouped send/recv when the devices are distinct GPUs — one xGMI link
-// per peer; a device-to-device copy when logical shards share a GPU) and are unpacked there.
-void Device::gather_local(const SlabLayout& base, int numTiles) {
+// per peer; hipMemcpyPeerAsync when ncclCommInitAll is unavailable; a device-to-device copy
+// when logical shards share a GPU) and are unpacked there. Every wait is bounded by
+// gatherTimeout; a timed-out RCCL gather aborts the communicators and later frames use peer
+// copies. Returns the YRT_GATHER_* path taken.
+int Device::gather_local(const SlabLayout& base, int numTiles) {
   const int N = (int)ctx.size();
   bool distinct = true;
   for (int a = 0; a < N; ++a)
@@ -746,16 +774,34 @@ void Device::gather_local(const SlabLayout& base, int numTiles) {
     HIP_CHECK(hipSetDevice(g0.hipDevice));
     g0.recvSlabs[k].alloc((size_t)std::max(1, tiles[k]) * 256 * eb);
   }
-  if (distinct) {
-    const RcclApi& nc = rccl();
-    if (!localComm) {
+  const Clock::time_point deadline =
+      Clock::now() + std::chrono::microseconds((long long)(gatherTimeout * 1e6));
+  auto wait_ctx = [&](int k, const char* phase) {
+    HIP_CHECK(hipSetDevice(ctx[k]->hipDevice));
+    if (!stream_wait_until(ctx[k]->stream, deadline))
+      throw std::runtime_error(std::string("multi-GPU gather: ") + phase + " on HIP device " +
+                               std::to_string(ctx[k]->hipDevice) + " timed out after " +
+                               std::to_string(gatherTimeout) + " s");
+  };
+  int path = distinct ? YRT_GATHER_RCCL_LOCAL : YRT_GATHER_D2D;
+  if (distinct && !localRcclOff && !localComm) {
+    try {
+      const RcclApi& nc = rccl();
       std::vector<int> devs;
       for (auto& g : ctx) devs.push_back(g->hipDevice);
       std::vector<ncclComm_t> comms(N);
       rccl_check(nc.CommInitAll(comms.data(), N, devs.data()), "ncclCommInitAll");
       localComms.assign(comms.begin(), comms.end());
       localComm = comms[0];
+    } catch (const std::exception& e) {
+      localRcclOff = true;
+      localRcclWhy = e.what();
+      fprintf(stderr, "yrt: %s; the multi-GPU gather uses hipMemcpyPeerAsync instead\n", e.what());
     }
+  }
+  if (distinct && localRcclOff) path = YRT_GATHER_PEER_COPY;
+  if (path == YRT_GATHER_RCCL_LOCAL) {
+    const RcclApi& nc = rccl();
     rccl_check(nc.GroupStart(), "ncclGroupStart");
     for (int k = 1; k < N; ++k) {
       const size_t bytes = (size_t)tiles[k] * 256 * eb;
@@ -766,7 +812,7 @@ void Device::gather_local(const SlabLayout& base, int numTiles) {
     rccl_check(nc.GroupEnd(), "ncclGroupEnd");
   } else {
     for (int k = 1; k < N; ++k) {
-      HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
+      wait_ctx(k, "tile pack");
       const size_t bytes = (size_t)tiles[k] * 256 * eb;
       if (bytes)
         HIP_CHECK(hipMemcpyPeerAsync(g0.recvSlabs[k].p, g0.hipDevice, ctx[k]->dSlab.p, ctx[k]->hipDevice, bytes,
@@ -777,29 +823,39 @@ void Device::gather_local(const SlabLayout& base, int numTiles) {
   for (int k = 1; k < N; ++k)
     launch_unpack_tiles(g0.recvSlabs[k].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), lay[k], tiles[k],
                         g0.stream);
-  for (int k = 0; k < N; ++k) {
-    HIP_CHECK(hipSetDevice(ctx[k]->hipDevice));
-    HIP_CHECK(hipStreamSynchronize(ctx[k]->stream));
+  try {
+    for (int k = 0; k < N; ++k) wait_ctx(k, path == YRT_GATHER_RCCL_LOCAL ? "RCCL slab send/recv" : "slab copy");
+  } catch (...) {
+    if (path == YRT_GATHER_RCCL_LOCAL) {
+      // the communicators may hold a send/recv that never matches: abort them and gather with
+      // peer copies from now on
+      try {
+        const RcclApi& nc = rccl();
+        for (auto c : localComms) (nc.CommAbort ? nc.CommAbort : nc.CommDestroy)(c);
+      } catch (...) {
+      }
+      localComms.clear();
+      localComm = nullptr;
+      localRcclOff = true;
+      localRcclWhy = "an RCCL gather timed out";
+    }
+    throw;
   }
   HIP_CHECK(hipSetDevice(g0.hipDevice));
+  return path;
 }
 
 // This process's tiles (shard shardIndex of shardCount, already gathered on ctx[0]) to rank 0
-// of the process communicator (yrtSetShardComm): the ranks first exchange their render status
-// (one 4-byte min all-reduce, so a rank whose render failed makes every rank fail instead of
-// leaving rank 0 waiting for its slab), then every rank packs its tiles and rank 0 receives
-// each peer's slab (grouped RCCL send/recv) and unpacks it into its frames.
+// of the process transport (gather.h: RCCL, yrtSetShardComm, or the in-process hub,
+// yrtSetShardHub): the ranks first exchange their render status (the min of every rank's
+// flag, so a rank whose render failed makes every rank fail instead of leaving rank 0 waiting
+// for its slab), then every rank packs its tiles and rank 0 receives each peer's slab and
+// unpacks it into its frames. Every wait is bounded by gatherTimeout.
 void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) {
-  const RcclApi& nc = rccl();
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   const int P = shardCount;
-  int flag = localOk ? 1 : 0;
-  dCommFlag.alloc(sizeof(int));
-  HIP_CHECK(hipMemcpyAsync(dCommFlag.p, &flag, sizeof(int), hipMemcpyHostToDevice, g0.stream));
-  rccl_check(nc.AllReduce(dCommFlag.p, dCommFlag.p, 1, ncclInt32, ncclMin, procComm, g0.stream), "ncclAllReduce");
-  HIP_CHECK(hipMemcpyAsync(&flag, dCommFlag.p, sizeof(int), hipMemcpyDeviceToHost, g0.stream));
-  HIP_CHECK(hipStreamSynchronize(g0.stream));
+  const int flag = proc->exchange_status(localOk ? 1 : 0, g0.hipDevice, g0.stream, gatherTimeout);
   if (!flag) {
     if (localOk) throw std::runtime_error("rtRenderFrame: a peer rank's render failed (no frame gathered)");
     return;  // the caller rethrows this rank's own error
@@ -812,27 +868,25 @@ void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) 
     const int tiles = shard_tiles(numTiles, shardIndex, P);
     g0.dSlab.alloc((size_t)std::max(1, tiles) * 256 * eb);
     launch_pack_tiles(g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles, g0.dSlab.p, g0.stream);
-    if (tiles)
-      rccl_check(nc.Send(g0.dSlab.p, (size_t)tiles * 256 * eb, ncclUint8, 0, procComm, g0.stream), "ncclSend");
+    proc->send_root(g0.dSlab.p, (size_t)tiles * 256 * eb, g0.hipDevice, g0.stream, gatherTimeout);
   } else {
     std::vector<int> tiles(P);
+    std::vector<void*> bufs(P, nullptr);
+    std::vector<size_t> bytes(P, 0);
     for (int r = 1; r < P; ++r) {
       tiles[r] = shard_tiles(numTiles, r, P);
       g0.recvSlabs[r].alloc((size_t)std::max(1, tiles[r]) * 256 * eb);
+      bufs[r] = g0.recvSlabs[r].p;
+      bytes[r] = (size_t)tiles[r] * 256 * eb;
     }
-    rccl_check(nc.GroupStart(), "ncclGroupStart");
-    for (int r = 1; r < P; ++r)
-      if (tiles[r])
-        rccl_check(nc.Recv(g0.recvSlabs[r].p, (size_t)tiles[r] * 256 * eb, ncclUint8, r, procComm, g0.stream),
-                   "ncclRecv");
-    rccl_check(nc.GroupEnd(), "ncclGroupEnd");
+    proc->recv_all(bufs, bytes, g0.hipDevice, g0.stream, gatherTimeout);
     for (int r = 1; r < P; ++r) {
       L.tileOffset = r;
       launch_unpack_tiles(g0.recvSlabs[r].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles[r],
                           g0.stream);
     }
+    HIP_CHECK(hipStreamSynchronize(g0.stream));
   }
-  HIP_CHECK(hipStreamSynchronize(g0.stream));
 }
 
 // ---------------------------------------------------------------- ray queries
@@ -1395,13 +1449,23 @@ int yrtCommit(YRTDevice dev, YRTHandle h) {
 int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene, YRTHandle tonemapper,
                    YRTHandle framebuffer, int accumulate) {
   DEV_GUARD(dev, -1)
-  auto R = dev->d->get<RendererObj>(renderer, "renderer");
-  auto C = dev->d->get<CameraObj>(camera, "camera");
-  auto S = dev->d->get<SceneObj>(scene, "scene");
-  auto T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
-  auto F = dev->d->get<FrameBufferObj>(framebuffer, "framebuffer");
-  if (!R || !C || !S || !T || !F) throw std::runtime_error("rtRenderFrame: null handle");
-  if (!dev->d->gpu) throw std::runtime_error("rtRenderFrame: host-only device (created with parms \"host\")");
+  std::shared_ptr<RendererObj> R;
+  std::shared_ptr<CameraObj> C;
+  std::shared_ptr<SceneObj> S;
+  std::shared_ptr<ToneMapperObj> T;
+  std::shared_ptr<FrameBufferObj> F;
+  try {
+    R = dev->d->get<RendererObj>(renderer, "renderer");
+    C = dev->d->get<CameraObj>(camera, "camera");
+    S = dev->d->get<SceneObj>(scene, "scene");
+    T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
+    F = dev->d->get<FrameBufferObj>(framebuffer, "framebuffer");
+    if (!R || !C || !S || !T || !F) throw std::runtime_error("rtRenderFrame: null handle");
+    if (!dev->d->gpu) throw std::runtime_error("rtRenderFrame: host-only device (created with parms \"host\")");
+  } catch (...) {
+    dev->d->fail_proc_gather();  // the peers of a process gather must not wait for this rank
+    throw;
+  }
   dev->d->render(*R, {C.get()}, *S, *T, {F.get()}, accumulate);
   return 0;
   DEV_END(-1)
@@ -1410,23 +1474,38 @@ int yrtRenderFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandl
 int yrtRenderFrames(YRTDevice dev, YRTHandle renderer, const YRTHandle* cameras, int numFrames, YRTHandle scene,
                     YRTHandle tonemapper, const YRTHandle* framebuffers, int accumulate) {
   DEV_GUARD(dev, -1)
-  if (numFrames < 1 || !cameras || !framebuffers) throw std::runtime_error("rtRenderFrames: no frames");
-  auto R = dev->d->get<RendererObj>(renderer, "renderer");
-  auto S = dev->d->get<SceneObj>(scene, "scene");
-  auto T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
-  if (!R || !S || !T) throw std::runtime_error("rtRenderFrames: null handle");
-  std::vector<std::shared_ptr<CameraObj>> cs(numFrames);
-  std::vector<std::shared_ptr<FrameBufferObj>> fs(numFrames);
-  std::vector<CameraObj*> cp(numFrames);
-  std::vector<FrameBufferObj*> fp(numFrames);
-  for (int k = 0; k < numFrames; ++k) {
-    cs[k] = dev->d->get<CameraObj>(cameras[k], "camera");
-    fs[k] = dev->d->get<FrameBufferObj>(framebuffers[k], "framebuffer");
-    if (!cs[k] || !fs[k]) throw std::runtime_error("rtRenderFrames: null camera or framebuffer handle");
-    cp[k] = cs[k].get();
-    fp[k] = fs[k].get();
+  std::shared_ptr<RendererObj> R;
+  std::shared_ptr<SceneObj> S;
+  std::shared_ptr<ToneMapperObj> T;
+  std::vector<std::shared_ptr<CameraObj>> cs;
+  std::vector<std::shared_ptr<FrameBufferObj>> fs;
+  std::vector<CameraObj*> cp;
+  std::vector<FrameBufferObj*> fp;
+  try {
+    if (numFrames < 1 || !cameras || !framebuffers) throw std::runtime_error("rtRenderFrames: no frames");
+    R = dev->d->get<RendererObj>(renderer, "renderer");
+    S = dev->d->get<SceneObj>(scene, "scene");
+    T = dev->d->get<ToneMapperObj>(tonemapper, "tonemapper");
+    if (!R || !S || !T) throw std::runtime_error("rtRenderFrames: null handle");
+    // one accumulation state per framebuffer and sampler iteration per job: a multi-frame job
+    // equals a loop of yrtRenderFrame calls only for non-accumulating frames (yrt_device.h)
+    if (numFrames > 1 && accumulate) throw std::runtime_error("rtRenderFrames: accumulate needs numFrames == 1");
+    cs.resize(numFrames);
+    fs.resize(numFrames);
+    cp.resize(numFrames);
+    fp.resize(numFrames);
+    for (int k = 0; k < numFrames; ++k) {
+      cs[k] = dev->d->get<CameraObj>(cameras[k], "camera");
+      fs[k] = dev->d->get<FrameBufferObj>(framebuffers[k], "framebuffer");
+      if (!cs[k] || !fs[k]) throw std::runtime_error("rtRenderFrames: null camera or framebuffer handle");
+      cp[k] = cs[k].get();
+      fp[k] = fs[k].get();
+    }
+    if (!dev->d->gpu) throw std::runtime_error("rtRenderFrames: host-only device (created with parms \"host\")");
+  } catch (...) {
+    dev->d->fail_proc_gather();
+    throw;
   }
-  if (!dev->d->gpu) throw std::runtime_error("rtRenderFrames: host-only device (created with parms \"host\")");
   dev->d->render(*R, cp, *S, *T, fp, accumulate);
   return 0;
   DEV_END(-1)
@@ -1675,12 +1754,12 @@ int yrtDebugPixelSamples(YRTDevice dev, int pixelId, int frame, float* out4, int
   // one capture at a time per process (the kernel-side target is a module global)
   DevBuf& buf = D.dbgPixelBuf;
   if (!out4) {
-    if (pixelId < 0) return debug_pixel_capture(-1, -1, nullptr);
+    if (pixelId < 0) return debug_pixel_capture(-1, -1, nullptr, 0);
     if (maxSamples < 1) throw std::runtime_error("yrtDebugPixelSamples: maxSamples < 1");
     buf.alloc((size_t)maxSamples * sizeof(float4));
     HIP_CHECK(hipMemset(buf.p, 0, (size_t)maxSamples * sizeof(float4)));
     D.dbgPixelCap = maxSamples;
-    return debug_pixel_capture(pixelId, frame, buf.as<float4>());
+    return debug_pixel_capture(pixelId, frame, buf.as<float4>(), maxSamples);
   }
   if (!buf.p) throw std::runtime_error("yrtDebugPixelSamples: no capture armed on this device");
   const int n = std::min(maxSamples, D.dbgPixelCap);
@@ -1704,10 +1783,10 @@ int yrtSetTileShard(YRTDevice dev, int index, int count) {
   if (count < 1 || index < 0 || index >= count) throw std::runtime_error("invalid shard");
   // a process communicator gathers exactly its own shard (rank of world): another shard would
   // post sends/receives its peers never match
-  if (dev->d->procComm && (index != dev->d->commRank || count != dev->d->commWorld))
+  if (dev->d->proc && (index != dev->d->commRank || count != dev->d->commWorld))
     throw std::runtime_error("yrtSetTileShard: shard differs from the process communicator's (rank " +
                              std::to_string(dev->d->commRank) + " of " + std::to_string(dev->d->commWorld) +
-                             "); call yrtSetShardComm(dev, 0, 1, id) first to drop it");
+                             "); call yrtSetShardComm(dev, 0, 1, id) or yrtSetShardHub(dev, NULL, 0) first to drop it");
   dev->d->shardIndex = index;
   dev->d->shardCount = count;
   return 0;
@@ -1739,15 +1818,12 @@ int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128) {
   Device& D = *dev->d;
   if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("invalid shard");
   if (!D.gpu) throw std::runtime_error("host-only device");
-  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
-  ncclUniqueId id;
-  memcpy(&id, id128, sizeof(id));
   HIP_CHECK(hipSetDevice(D.hipDevice));
-  if (D.procComm) rccl().CommDestroy(D.procComm), D.procComm = nullptr;
+  D.proc.reset();
   D.commRank = 0;
   D.commWorld = 1;
   if (world > 1) {
-    rccl_check(rccl().CommInitRank(&D.procComm, world, id, rank), "ncclCommInitRank");
+    D.proc = make_rccl_transport(rank, world, id128);
     D.commRank = rank;
     D.commWorld = world;
   }
@@ -1756,6 +1832,79 @@ int yrtSetShardComm(YRTDevice dev, int rank, int world, const void* id128) {
   return 0;
   DEV_END(-1)
 }
+
+struct YRTShardHub_ {
+  std::shared_ptr<ShardHub> hub;
+};
+static thread_local std::string t_hubError;
+
+YRTShardHub yrtNewShardHub(int world) {
+  try {
+    auto* h = new YRTShardHub_;
+    h->hub = make_shard_hub(world);
+    return h;
+  } catch (const std::exception& e) {
+    t_hubError = e.what();
+    return nullptr;
+  }
+}
+
+void yrtDeleteShardHub(YRTShardHub hub) { delete hub; }
+
+int yrtSetShardHub(YRTDevice dev, YRTShardHub hub, int rank) {
+  DEV_GUARD(dev, -1)
+  Device& D = *dev->d;
+  D.proc.reset();
+  D.commRank = 0;
+  D.commWorld = 1;
+  D.shardIndex = 0;
+  D.shardCount = 1;
+  if (!hub) return 0;
+  const int world = shard_hub_world(*hub->hub);
+  if (rank < 0 || rank >= world) throw std::runtime_error("yrtSetShardHub: invalid rank");
+  if (!D.gpu && world > 1) throw std::runtime_error("host-only device");
+  if (world > 1) {
+    D.proc = make_hub_transport(hub->hub, rank);
+    D.commRank = rank;
+    D.commWorld = world;
+  }
+  D.shardIndex = rank;
+  D.shardCount = world;
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtSetGatherTimeout(YRTDevice dev, double seconds) {
+  DEV_GUARD(dev, -1)
+  if (!(seconds > 0)) throw std::runtime_error("yrtSetGatherTimeout: seconds must be > 0");
+  dev->d->gatherTimeout = seconds;
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtShardHubStatus(YRTShardHub hub, int rank, int flag, double timeoutS) {
+  try {
+    if (!hub) throw std::runtime_error("null hub");
+    return hub_host_status(*hub->hub, rank, flag, timeoutS);
+  } catch (const std::exception& e) {
+    t_hubError = e.what();
+    return -1;
+  }
+}
+
+int yrtShardHubSlab(YRTShardHub hub, int rank, const void* slab, size_t bytes, void* recv, size_t recvBytesPerRank,
+                    double timeoutS) {
+  try {
+    if (!hub) throw std::runtime_error("null hub");
+    hub_host_slab(*hub->hub, rank, slab, bytes, recv, recvBytesPerRank, timeoutS);
+    return 0;
+  } catch (const std::exception& e) {
+    t_hubError = e.what();
+    return -1;
+  }
+}
+
+const char* yrtShardHubLastError(void) { return t_hubError.c_str(); }
 
 int yrtGetDeviceCount(YRTDevice dev) {
   DEV_GUARD(dev, -1)

@@ -33,6 +33,9 @@ const RcclApi& rccl() {
     api.CommInitRank = (decltype(api.CommInitRank))sym("ncclCommInitRank");
     api.CommInitAll = (decltype(api.CommInitAll))sym("ncclCommInitAll");
     api.CommDestroy = (decltype(api.CommDestroy))sym("ncclCommDestroy");
+    // abort and async-error polling bound the gather's waits (gather.cpp); optional
+    api.CommAbort = (decltype(api.CommAbort))dlsym(h, "ncclCommAbort");
+    api.CommGetAsyncError = (decltype(api.CommGetAsyncError))dlsym(h, "ncclCommGetAsyncError");
     api.GroupStart = (decltype(api.GroupStart))sym("ncclGroupStart");
     api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
     api.Send = (decltype(api.Send))sym("ncclSend");

@@ -20,6 +20,8 @@ struct RcclApi {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
   ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*);
   ncclResult_t (*CommDestroy)(ncclComm_t);
+  ncclResult_t (*CommAbort)(ncclComm_t);                         // optional (nullptr: CommDestroy)
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*);  // optional
   ncclResult_t (*GroupStart)();
   ncclResult_t (*GroupEnd)();
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);

@@ -14,6 +14,10 @@
 // Wave64: every cross-lane primitive below is written for 64 lanes (ballot is 64-bit).
 
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <mutex>
+#include <set>
 
 #include "yrt_kernels.h"
 #include "yrt_shade.h"
@@ -438,7 +442,9 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 
 // MOTION: moving geometry; rayTime[q] is query q's time (Ray::time, set from sample.getTime()
 // for camera rays and inherited by shadow and continuation rays, pathtraceintegrator.cpp:158,210)
-template <bool ANY, bool MOTION>
+// WIDE (any-hit only): node steps on the 8-wide BVH (sv.nodes8, GpuNode8): the farthest hit
+// child next, the other hit ones pushed — fewer, wider steps per query
+template <bool ANY, bool MOTION, bool WIDE = false>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
@@ -606,6 +612,33 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       YRT_PROF(2, 1);
       YRT_PROF(3, __popcll(ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
+       if constexpr (WIDE) {
+        float t[8];
+        int c[8];
+        box8_any(sv.nodes8, curIdx, __float_as_int(ri.w), r, best.t, t, c);
+        far8(t, c);
+        const float MISS = __int_as_float(0xff800000);
+        if (sp + 7 <= kLds) {
+          // unconditional stores into free ring slots, sp advanced past the hit ones (as below)
+          int o = sp;
+#pragma unroll
+          for (int k = 7; k >= 1; --k) {
+            stack[YRT_SLOT(o)] = c[k];
+            o += t[k] > MISS ? 1 : 0;
+          }
+          sp = o;
+        } else {
+#pragma unroll
+          for (int k = 7; k >= 1; --k)
+            if (t[k] > MISS) YRT_PUSH(c[k]);
+        }
+        if (t[0] > MISS) {
+          curIdx = c[0] >> 5;
+          curCnt = c[0] & 31;
+        } else {
+          YRT_POP();
+        }
+       } else {
         float t[4];
         int c[4];
         // sign-ordered slab planes (+1.5 % on C3 with two lanes, bit-identical distances)
@@ -638,6 +671,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
 #undef YRT_HIT
+       }
         if (curCnt > 0 && pendCnt == 0) {
           pendIdx = curIdx;
           pendCnt = curCnt;
@@ -1537,7 +1571,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_shadow_resolve(PathBuffers pb, in
 
 // Debug capture (yrtDebugPixelSamples): the per-sample radiance of one pixel of one frame,
 // in the pixel's summation order, for parity debugging against oracle_debug_pixel.
-__device__ int g_dbgPixel[2] = {-1, -1};  // pixel id (y * width + x), frame
+__device__ int g_dbgPixel[3] = {-1, -1, 0};  // pixel id (y * width + x), frame, capacity of g_dbgOut
 __device__ float4* g_dbgOut = nullptr;
 
 // AccuBuffer::update (api/framebuffer.h:289-304) + DefaultToneMapper::eval
@@ -1556,7 +1590,7 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_resolve_pixels(FrameView fv, Path
       L = L + v3(l4.x, l4.y, l4.z);
     }
     if (g_dbgPixel[0] == y * rp.width + x && g_dbgPixel[1] == f && g_dbgOut)
-      for (int s = 0; s < rp.spp; ++s) g_dbgOut[s] = pb.pathL[(size_t)s * bi.numPixels + i];
+      for (int s = 0; s < min(rp.spp, g_dbgPixel[2]); ++s) g_dbgOut[s] = pb.pathL[(size_t)s * bi.numPixels + i];
     // AccuBuffer::update: non-accumulating frames store (L, spp), accumulating ones add
     const size_t pix = (size_t)f * frameStride + (size_t)y * rp.width + x;
     float4 a = make_float4(L.x, L.y, L.z, (float)rp.spp);
@@ -1707,13 +1741,23 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
                       const float* time) {
   const long long maxCount = hinted((long long)numSegs * segCap, countHint);
   const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
-  if (time)
-    hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
-                       (float4*)nullptr, occluded, sv.traceSpill, fuse ? *fuse : ShadowFuse{}, time);
-  else
-    hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                       segCap, (float4*)nullptr, occluded, sv.traceSpill, fuse ? *fuse : ShadowFuse{},
-                       (const float*)nullptr);
+  const ShadowFuse sf = fuse ? *fuse : ShadowFuse{};
+  // the 8-wide BVH when the scene has one (scene_gpu.cpp: YRT_ANY_BVH8, the stack bound)
+  if (time) {
+    if (sv.nodes8)
+      hipLaunchKernelGGL((k_trace<true, true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
+                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time);
+    else
+      hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time);
+  } else {
+    if (sv.nodes8)
+      hipLaunchKernelGGL((k_trace<true, false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
+                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr);
+    else
+      hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr);
+  }
 }
 
 // Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of
@@ -1758,7 +1802,23 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
     case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s, countHint); break;
     case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s, countHint); break;
     case YRT_SV_COLLADA: launch_shade_t<YRT_SV_COLLADA>(sv, fv, pb, bi, depth, s, countHint); break;
-    default: launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s, countHint); break;
+    default: {
+      // the generic kernel (every material and light type) holds ~218 VGPRs, 2 waves/SIMD:
+      // say so once per material set, so a scene outside the specialized sets is not slow
+      // without a trace
+      static std::mutex mu;
+      static std::set<unsigned> warned;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (warned.insert(materialMask).second)
+          fprintf(stderr,
+                  "yrt: material/light set 0x%x has no specialized k_shade; using the generic kernel "
+                  "(2 waves/SIMD, slower shading)\n",
+                  materialMask);
+      }
+      launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s, countHint);
+      break;
+    }
   }
 }
 
@@ -1907,8 +1967,8 @@ int check_math(int fn, unsigned long long* host2) {
   return rc;
 }
 
-int debug_pixel_capture(int pixelId, int frame, float4* out) {
-  const int v[2] = {pixelId, frame};
+int debug_pixel_capture(int pixelId, int frame, float4* out, int capacity) {
+  const int v[3] = {pixelId, frame, out ? capacity : 0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbgPixel), v, sizeof(v)) != hipSuccess) return -1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_dbgOut), &out, sizeof(out)) != hipSuccess) return -1;
   return 0;
@@ -2031,6 +2091,28 @@ void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices,
   if (count <= 0) return;
   hipLaunchKernelGGL(k_refit_nodes, dim3((count + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes, tris,
                      indices, positions, levelNodes, count);
+}
+
+// the 8-wide any-hit BVH after a 4-wide refit: every child box is a 4-wide node's child box
+__global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes8(GpuNode8* __restrict__ nodes8,
+                                                           const GpuNode* __restrict__ nodes,
+                                                           const int* __restrict__ src, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count * 8) return;
+  const int s = src[i];
+  if (s < 0) return;  // empty slot: its inverted box stays
+  const GpuNode& n = nodes[s >> 2];
+  const int q = s & 3, j = i & 7;
+  GpuNode8& o = nodes8[i >> 3];
+  o.lox[j] = n.lox[q]; o.hix[j] = n.hix[q];
+  o.loy[j] = n.loy[q]; o.hiy[j] = n.hiy[q];
+  o.loz[j] = n.loz[q]; o.hiz[j] = n.hiz[q];
+}
+
+void launch_refit_nodes8(GpuNode8* nodes8, const GpuNode* nodes, const int* src, int numNodes8, hipStream_t s) {
+  if (numNodes8 <= 0) return;
+  hipLaunchKernelGGL(k_refit_nodes8, dim3((numNodes8 * 8 + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes8,
+                     nodes, src, numNodes8);
 }
 
 }  // namespace yrt

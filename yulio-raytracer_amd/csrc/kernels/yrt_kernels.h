@@ -12,6 +12,7 @@ namespace yrt {
 
 struct SceneView {
   const GpuNode* nodes;
+  const GpuNode8* nodes8;  // the any-hit traversal's 8-wide BVH (null: any-hit uses nodes)
   const GpuTri* tris;
   const int* triGeom;
   const int4* indices;
@@ -146,7 +147,7 @@ void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const Bat
 int trace_profile(unsigned long long* out8, int reset);
 // Debug capture: per-sample radiance of pixel id (y * width + x) of frame `frame` written to
 // out[s] by the next resolves (pixelId -1: off)
-int debug_pixel_capture(int pixelId, int frame, float4* out);
+int debug_pixel_capture(int pixelId, int frame, float4* out, int capacity);
 // Arithmetic self-check of the correctly rounded fast reciprocal (rcp_rn): see pathtrace.hip
 int check_math(int fn, unsigned long long* host2);
 // Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (job tile =
@@ -173,6 +174,8 @@ void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices,
                        hipStream_t s);
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
                         const int* levelNodes, int count, hipStream_t s);
+// 8-wide nodes: child s of node n takes the box of 4-wide (src[8n+s] >> 2, src[8n+s] & 3)
+void launch_refit_nodes8(GpuNode8* nodes8, const GpuNode* nodes, const int* src, int numNodes8, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 

@@ -397,6 +397,59 @@ class Device:
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._rc(N.dev.yrtSetShardComm(self.h, int(rank), int(world), buf), "set_shard_comm")
 
+    def set_shard_hub(self, hub, rank):
+        """Arms rank `rank` of an in-process ShardHub (yrtSetShardHub): tiles dealt round-robin
+        over the hub's devices, every frame gathered on rank 0's device inside rtRenderFrame
+        (the process gather's bookkeeping with peer / device-to-device copies). hub=None disarms."""
+        self._rc(N.dev.yrtSetShardHub(self.h, hub.h if hub is not None else None, int(rank)), "set_shard_hub")
+
+    def set_gather_timeout(self, seconds):
+        """Bound of every wait of a multi-GPU gather (yrtSetGatherTimeout)."""
+        self._rc(N.dev.yrtSetGatherTimeout(self.h, float(seconds)), "set_gather_timeout")
+
+
+GATHER_PATHS = {0: "none", 1: "d2d", 2: "rccl-local", 3: "peer-copy", 4: "rccl-process", 5: "hub"}
+
+
+class ShardHub:
+    """The in-process meeting point of a multi-device gather (yrtNewShardHub). status() and
+    slab() drive its two phases on host memory (CPU tests of the deadlines and size checks)."""
+
+    def __init__(self, world):
+        self.h = N.dev.yrtNewShardHub(int(world))
+        if not self.h:
+            raise RuntimeError(f"yrtNewShardHub: {N.dev.yrtShardHubLastError().decode()}")
+        self.world = int(world)
+
+    def close(self):
+        if self.h:
+            N.dev.yrtDeleteShardHub(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def status(self, rank, flag, timeout):
+        """Min of every rank's flag; raises RuntimeError (naming the missing ranks) on timeout."""
+        r = N.dev.yrtShardHubStatus(self.h, int(rank), int(flag), float(timeout))
+        if r < 0:
+            raise RuntimeError(N.dev.yrtShardHubLastError().decode())
+        return r
+
+    def slab(self, rank, data=b"", recv_bytes_per_rank=0, timeout=10.0):
+        """rank > 0 sends `data` to rank 0; rank 0 returns the peers' slabs (rank order)."""
+        src = np.frombuffer(bytes(data), np.uint8) if len(data) else np.zeros(1, np.uint8)
+        out = np.zeros(max(1, (self.world - 1) * recv_bytes_per_rank), np.uint8) if rank == 0 else None
+        r = N.dev.yrtShardHubSlab(self.h, int(rank), src.ctypes.data, len(data),
+                                  out.ctypes.data if out is not None else None, int(recv_bytes_per_rank),
+                                  float(timeout))
+        if r < 0:
+            raise RuntimeError(N.dev.yrtShardHubLastError().decode())
+        return out[:(self.world - 1) * recv_bytes_per_rank] if out is not None else None
+
 
 def sample_table(spp, sets, iteration, num1D, num2D, filter="bspline"):
     """Host sampler's SoA table (dims x records), see yrtDebugSampleTable."""

@@ -43,7 +43,7 @@ PF = C.POINTER(C.c_float)
 class RenderStats(C.Structure):
     _fields_ = [(n, C.c_double) for n in (
         "raysClosest", "raysShadow", "samples", "msTotal", "msTraceClosest", "msTraceShadow", "msShade",
-        "msOther", "launchesClosest", "launchesShadow", "nodeVisits", "triVisits")]
+        "msOther", "launchesClosest", "launchesShadow", "nodeVisits", "triVisits", "gather")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -147,6 +147,13 @@ _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
 _sig(dev, "yrtShardCommUniqueId", i32, vp)
 _sig(dev, "yrtSetShardComm", i32, vp, i32, i32, vp)
 _sig(dev, "yrtRcclAvailable", i32)
+_sig(dev, "yrtNewShardHub", vp, i32)
+_sig(dev, "yrtDeleteShardHub", None, vp)
+_sig(dev, "yrtSetShardHub", i32, vp, vp, i32)
+_sig(dev, "yrtSetGatherTimeout", i32, vp, C.c_double)
+_sig(dev, "yrtShardHubStatus", i32, vp, i32, i32, C.c_double)
+_sig(dev, "yrtShardHubSlab", i32, vp, i32, vp, sz, vp, sz, C.c_double)
+_sig(dev, "yrtShardHubLastError", cstr)
 _sig(dev, "yrtGetDeviceCount", i32, vp)
 _sig(dev, "yrtSetRefitCommits", i32, vp, i32)
 _sig(dev, "yrtGetSceneRefits", i32, vp, vp)
