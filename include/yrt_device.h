@@ -16,7 +16,10 @@
  *     crosses the ABI.
  *   - Every call on one device is serialized by a device mutex (singleray_device.cpp:97).
  *   - yrtRenderFrame is synchronous (integratorrenderer.cpp:90-93); yrtMapFrameBuffer
- *     returns the host pixel pointer (singleray_device.cpp:439-447).
+ *     returns the host pixel pointer (singleray_device.cpp:439-447). The frame stays in HBM
+ *     until the first yrtMapFrameBuffer of that buffer copies it to the host pixels (every
+ *     read of the pixels goes through the map, as in the reference); framebuffers created
+ *     over user pointers (yrtNewFrameBuffer ptrs) receive the pixels at the end of the render.
  */
 #ifndef YRT_DEVICE_H
 #define YRT_DEVICE_H
@@ -262,7 +265,9 @@ YRT_API int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2);
 /* Parity debugging: out4 == NULL arms the capture of the per-sample radiance (the pathL terms
  * the resolve sums, in s order) of pixel id y*width+x (-1 disarms) of frame `frame` for the
  * following renders (buffer of maxSamples float4); out4 != NULL copies the captured samples
- * and returns their count. Compare with oracle_debug_pixel. */
+ * and returns their count (at most maxSamples: the kernel writes no more than the buffer
+ * holds). Captures on the device's first GPU only (a multi-GPU device's other GPUs render
+ * their tiles uncaptured). Compare with oracle_debug_pixel. */
 YRT_API int yrtDebugPixelSamples(YRTDevice dev, int pixelId, int frame, float* out4, int maxSamples);
 /* Decoder check: 8-bit pixels of a .jpg/.png in file row order (top row first), before the
  * Image4c flip/requantization of rtNewImageFromFile. Call with out=NULL to get the size. */

@@ -427,3 +427,26 @@ def test_debug_pixel_samples_match_oracle(gpu_device):
             fresh.debug_pixel_samples(4)
     finally:
         fresh.close()
+
+
+@pytest.mark.gpu
+def test_framebuffer_read_back_at_map(gpu_device):
+    """rtRenderFrame leaves the frame in HBM and rtMapFrameBuffer reads it back on first access
+    (device.cpp fb_read_back): frames rendered into several framebuffers before any map — the
+    frame blocks ping-pong, a third live one is allocated, a re-rendered framebuffer drops its
+    older frame — all read back equal to frames mapped right after their render."""
+    s = yrt.Session(c4_args(64, 2) + ["-fb", "RGB_FLOAT32"], device=gpu_device)
+    i = s.info()
+    R, S, T = i["renderer"], i["scene"], i["tonemapper"]
+    ref = {f: s.render(f) for f in (0, 5, 9)}
+    d = gpu_device
+    fa, fb, fc = (d.rtNewFrameBuffer("RGB_FLOAT32", 64, 64) for _ in range(3))
+    d.rtRenderFrame(R, s.camera(0), S, T, fa, 0)
+    d.rtRenderFrame(R, s.camera(5), S, T, fb, 0)
+    d.rtRenderFrame(R, s.camera(9), S, T, fa, 0)
+    d.rtRenderFrame(R, s.camera(0), S, T, fc, 0)
+    assert np.array_equal(d.framebuffer_array(fa, 64, 64, "RGB_FLOAT32"), ref[9])
+    assert np.array_equal(d.framebuffer_array(fb, 64, 64, "RGB_FLOAT32"), ref[5])
+    assert np.array_equal(d.framebuffer_array(fc, 64, 64, "RGB_FLOAT32"), ref[0])
+    assert np.array_equal(d.framebuffer_array(fa, 64, 64, "RGB_FLOAT32"), ref[9])  # a second map: same pixels
+    s.close()

@@ -8,8 +8,11 @@
  * changes which triangle the next ray hits often enough to move whole pixels. Using these
  * functions on both sides (a documented substitution, like rcp/rsqrt -> IEEE)
  * makes the device's arithmetic reproducible by the oracle bit for bit. Both sides are built
- * with -ffp-contract=off (no fused multiply-add), IEEE round-to-nearest, correctly rounded
- * division and square root, so the same source gives the same bits.
+ * with -ffp-contract=off (no implicit fused multiply-add), IEEE round-to-nearest, correctly
+ * rounded division and square root; the polynomials and reductions here use explicit fused
+ * multiply-adds (YRT_LM_FMA: v_fma_f32 on the GPU, the FMA3 instruction or C99 fmaf in the
+ * oracle — one correctly rounded operation on both sides), so the same source gives the same
+ * bits with half the operations of separate multiplies and adds.
  *
  * Algorithms: Cody-Waite range reduction + minimax polynomials of the Cephes single-precision
  * library (sinf/cosf, expf, logf, asinf, atanf; S. L. Moshier, public domain), accurate to
@@ -40,6 +43,7 @@ YRT_LIBM_FN float yrt_lm_float(uint32_t u) {
   return f;
 }
 YRT_LIBM_FN float yrt_lm_floor(float x) { return __builtin_floorf(x); }
+#define YRT_LM_FMA(a, b, c) __builtin_fmaf((a), (b), (c))
 YRT_LIBM_FN float yrt_lm_sqrt(float x) { return __builtin_sqrtf(x); }
 
 /* 2^n for integer n in [-252, 254] as a product of two exact powers of two */
@@ -55,16 +59,18 @@ YRT_LIBM_FN float yrt_lm_ldexp(float x, int n) {
 /* ---- sin / cos: x = q * pi/2 + r, |r| <= pi/4 (three-part Cody-Waite pi/2) */
 YRT_LIBM_FN float yrt_lm_sin_poly(float r) {
   const float z = r * r;
-  return ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
+  const float p = YRT_LM_FMA(YRT_LM_FMA(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  return YRT_LM_FMA(p * z, r, r);
 }
 YRT_LIBM_FN float yrt_lm_cos_poly(float r) {
   const float z = r * r;
-  return ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z - 0.5f * z + 1.0f;
+  const float p = YRT_LM_FMA(YRT_LM_FMA(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+  return YRT_LM_FMA(p, z * z, YRT_LM_FMA(-0.5f, z, 1.0f));
 }
 YRT_LIBM_FN float yrt_lm_reduce(float x, int* quadrant) {
-  const float q = yrt_lm_floor(x * 0.636619772367581343f + 0.5f);
+  const float q = yrt_lm_floor(YRT_LM_FMA(x, 0.636619772367581343f, 0.5f));
   *quadrant = (int)q & 3;
-  return ((x - q * 1.5703125f) - q * 4.837512969970703125e-4f) - q * 7.54978995489188216e-8f;
+  return YRT_LM_FMA(-q, 7.54978995489188216e-8f, YRT_LM_FMA(-q, 4.837512969970703125e-4f, YRT_LM_FMA(-q, 1.5703125f, x)));
 }
 YRT_LIBM_FN float yrt_sinf(float x) {
   int k;
@@ -84,11 +90,15 @@ YRT_LIBM_FN float yrt_expf(float x) {
   if (x != x) return x;
   if (x > 88.72283905206835f) return yrt_lm_float(0x7f800000u);
   if (x < -103.97208f) return 0.0f;
-  const float n = yrt_lm_floor(1.44269504088896341f * x + 0.5f);
-  const float r = (x - n * 0.693359375f) - n * -2.12194440e-4f;
+  const float n = yrt_lm_floor(YRT_LM_FMA(1.44269504088896341f, x, 0.5f));
+  const float r = YRT_LM_FMA(n, 2.12194440e-4f, YRT_LM_FMA(-n, 0.693359375f, x));
   const float z = r * r;
-  const float p = (((((1.9875691500e-4f * r + 1.3981999507e-3f) * r + 8.3334519073e-3f) * r + 4.1665795894e-2f) * r +
-                    1.6666665459e-1f) * r + 5.0000001201e-1f) * z + r + 1.0f;
+  float q = YRT_LM_FMA(1.9875691500e-4f, r, 1.3981999507e-3f);
+  q = YRT_LM_FMA(q, r, 8.3334519073e-3f);
+  q = YRT_LM_FMA(q, r, 4.1665795894e-2f);
+  q = YRT_LM_FMA(q, r, 1.6666665459e-1f);
+  q = YRT_LM_FMA(q, r, 5.0000001201e-1f);
+  const float p = YRT_LM_FMA(q, z, r) + 1.0f;
   return yrt_lm_ldexp(p, (int)n);
 }
 
@@ -112,13 +122,18 @@ YRT_LIBM_FN float yrt_logf(float x) {
     m = m - 1.0f;
   }
   const float z = m * m;
-  float y = ((((((((7.0376836292e-2f * m - 1.1514610310e-1f) * m + 1.1676998740e-1f) * m - 1.2420140846e-1f) * m +
-                 1.4249322787e-1f) * m - 1.6668057665e-1f) * m + 2.0000714765e-1f) * m - 2.4999993993e-1f) * m +
-             3.3333331174e-1f) * m * z;
+  float q = YRT_LM_FMA(7.0376836292e-2f, m, -1.1514610310e-1f);
+  q = YRT_LM_FMA(q, m, 1.1676998740e-1f);
+  q = YRT_LM_FMA(q, m, -1.2420140846e-1f);
+  q = YRT_LM_FMA(q, m, 1.4249322787e-1f);
+  q = YRT_LM_FMA(q, m, -1.6668057665e-1f);
+  q = YRT_LM_FMA(q, m, 2.0000714765e-1f);
+  q = YRT_LM_FMA(q, m, -2.4999993993e-1f);
+  q = YRT_LM_FMA(q, m, 3.3333331174e-1f);
   const float fe = (float)e;
-  y += -2.12194440e-4f * fe;
-  y += -0.5f * z;
-  return (m + y) + 0.693359375f * fe;
+  float y = YRT_LM_FMA(-2.12194440e-4f, fe, q * m * z);
+  y = YRT_LM_FMA(-0.5f, z, y);
+  return YRT_LM_FMA(0.693359375f, fe, m + y);
 }
 
 /* ---- pow for the renderer's domain (x >= 0): BRDF exponents, medium depths, gamma */
@@ -131,6 +146,12 @@ YRT_LIBM_FN float yrt_powf(float x, float y) {
 }
 
 /* ---- asin / acos */
+YRT_LIBM_FN float yrt_lm_asin_poly(float z) {
+  float q = YRT_LM_FMA(4.2163199048e-2f, z, 2.4181311049e-2f);
+  q = YRT_LM_FMA(q, z, 4.5470025998e-2f);
+  q = YRT_LM_FMA(q, z, 7.4953002686e-2f);
+  return YRT_LM_FMA(q, z, 1.6666752422e-1f);
+}
 YRT_LIBM_FN float yrt_lm_asin_core(float a /* |x| */) {
   float z, v;
   int big = a > 0.5f;
@@ -141,8 +162,7 @@ YRT_LIBM_FN float yrt_lm_asin_core(float a /* |x| */) {
     z = a * a;
     v = a;
   }
-  float r = ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
-             1.6666752422e-1f) * z * v + v;
+  float r = YRT_LM_FMA(yrt_lm_asin_poly(z) * z, v, v);
   if (big) r = 1.5707963267948966192f - (r + r);
   return r;
 }
@@ -161,8 +181,7 @@ YRT_LIBM_FN float yrt_acosf(float x) {
   const float w = yrt_lm_sqrt(0.5f * (hi ? 1.0f - x : 1.0f + x));
   const float a = (lo || hi) ? w : (x < 0.0f ? -x : x);
   const float z = a * a;
-  const float r = ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
-                   1.6666752422e-1f) * z * a + a;
+  const float r = YRT_LM_FMA(yrt_lm_asin_poly(z) * z, a, a);
   if (lo) return 3.14159265358979323846f - 2.0f * r;
   if (hi) return 2.0f * r;
   return 1.5707963267948966192f - (x < 0.0f ? -r : r);
@@ -184,7 +203,10 @@ YRT_LIBM_FN float yrt_atanf(float x) {
     t = a;
   }
   const float z = t * t;
-  y += (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * t + t;
+  float q = YRT_LM_FMA(8.05374449538e-2f, z, -1.38776856032e-1f);
+  q = YRT_LM_FMA(q, z, 1.99777106478e-1f);
+  q = YRT_LM_FMA(q, z, -3.33329491539e-1f);
+  y += YRT_LM_FMA(q * z, t, t);
   return x < 0.0f ? -y : y;
 }
 YRT_LIBM_FN float yrt_atan2f(float y, float x) {

@@ -52,7 +52,7 @@ struct GpuCtx {
   // latency-bound shading).
   struct Lane {
     hipStream_t stream = nullptr;
-    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
+    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, sIdx, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
     int64_t pathCap = 0, shadowCap = 0;
     unsigned* hc = nullptr;  // pinned copy of the counters of the lane's last batch
@@ -61,10 +61,20 @@ struct GpuCtx {
     int64_t pendTiles = 0;   // tiles done once that batch drains (progress)
     std::vector<int64_t> pendFrameTiles;  // that batch's tiles per frame (grid-size hints)
   };
-  static constexpr int kMaxLanes = 2;
+  static constexpr int kMaxLanes = 4;      // YRT_LANES may ask for up to 4 (the sweeps of DESIGN §3)
+  static constexpr int kDefaultLanes = 2;  // two: C3 +4 % over one, three or four no better
   Lane lanes[kMaxLanes];
-  int numLanes = kMaxLanes;
-  DevBuf dRp, dCam, dPixelSets, dFbFloat, dFbRGB8, dAccu, dCount, dSpill, dSlab, dDirect;
+  int numLanes = kDefaultLanes;
+  DevBuf dRp, dCam, dPixelSets, dAccu, dCount, dSpill, dSlab, dDirect;
+  // The frames a job renders into (float RGB and RGB8 rows, frame-major). On the primary
+  // device a job's framebuffers keep a reference to their block until rtMapFrameBuffer reads
+  // them back, so the next job renders into the spare (or a fresh) block meanwhile.
+  struct FrameBlock {
+    DevBuf fbFloat, fbRGB8;
+  };
+  std::shared_ptr<FrameBlock> blk = std::make_shared<FrameBlock>(), spareBlk;
+  float* fbFloat() const { return blk->fbFloat.as<float>(); }
+  uint8_t* fbRGB8() const { return blk->fbRGB8.as<uint8_t>(); }
   std::vector<int> hDirect;        // the frame's direct-light list (uploaded to dDirect)
   std::vector<GpuCamera> hCams;  // the job's cameras, one per frame (uploaded to dCam)
   DevBuf dBackplate;                       // the renderer's backplate image (texels)
@@ -124,6 +134,7 @@ struct GpuCtx {
       L.sDir.alloc(S * 16);
       L.sContrib.alloc(S * 16);
       L.sOcc.alloc(S * 4);
+      L.sIdx.alloc(S * 4);
       L.shadowCap = S;
     }
     if (motion) {
@@ -201,7 +212,7 @@ class Device {
   bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
   Device(const std::vector<int>& devs, bool useGpu) : gpu(useGpu) {
     if (!gpu) return;
-    int lanes = GpuCtx::kMaxLanes;
+    int lanes = GpuCtx::kDefaultLanes;
     if (const char* e = getenv("YRT_LANES")) lanes = std::max(1, std::min(GpuCtx::kMaxLanes, atoi(e)));
     for (int d : devs) ctx.emplace_back(new GpuCtx(d, lanes));
     hipDevice = ctx[0]->hipDevice;
@@ -285,6 +296,39 @@ static void status(RendererObj& R, int state, float progress) {
   if (R.statusCallback) ((YRTStatusCallback)R.statusCallback)(state, progress, R.statusUser);
 }
 
+// Copies the frame framebuffer F's buffer `id` still holds in HBM (FrameBufferObj::Pending)
+// into its host pixels, converting float RGB to the RGBA / RGBA8 formats.
+void fb_read_back(FrameBufferObj& F, int id) {
+  if (id < 0 || id >= (int)F.pending.size() || !F.pending[id].keep) return;
+  FrameBufferObj::Pending pf = F.pending[id];
+  F.pending[id] = FrameBufferObj::Pending();
+  HIP_CHECK(hipSetDevice(pf.hipDevice));
+  const int W = F.width, H = F.height;
+  void* dst = F.buffer(id);
+  if (F.format == FB_RGB8) {
+    HIP_CHECK(hipMemcpy(dst, pf.src, F.stride * H, hipMemcpyDeviceToHost));
+    return;
+  }
+  if (F.format == FB_RGB_FLOAT32) {
+    HIP_CHECK(hipMemcpy(dst, pf.src, (size_t)W * H * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    return;
+  }
+  std::vector<float> tmp((size_t)W * H * 3);
+  HIP_CHECK(hipMemcpy(tmp.data(), pf.src, tmp.size() * sizeof(float), hipMemcpyDeviceToHost));
+  if (F.format == FB_RGBA_FLOAT32) {
+    float* o = (float*)dst;
+    for (size_t i = 0; i < (size_t)W * H; ++i) {
+      o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
+    }
+  } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
+    uint8_t* o = (uint8_t*)dst;
+    for (size_t i = 0; i < (size_t)W * H; ++i) {
+      for (int c = 0; c < 3; ++c) o[4 * i + c] = (uint8_t)clampf(tmp[3 * i + c] * 255.0f, 0.0f, 255.0f);
+      o[4 * i + 3] = 0;
+    }
+  }
+}
+
 void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& S, ToneMapperObj& T,
                     const std::vector<FrameBufferObj*>& F, int accumulate) {
   auto t0 = std::chrono::steady_clock::now();
@@ -324,6 +368,14 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     }
     memset(&stats, 0, sizeof(stats));
     if (!accumulate) R.iteration = 0;
+    {
+      // frames of an earlier job not yet read back: this job renders into another block
+      GpuCtx& g0 = *ctx[0];
+      if (g0.blk.use_count() > 1) {
+        std::swap(g0.blk, g0.spareBlk);
+        if (!g0.blk || g0.blk.use_count() > 1) g0.blk = std::make_shared<GpuCtx::FrameBlock>();
+      }
+    }
     std::vector<GpuScene*> scenes(nr);
     for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
     if (nr == 1) {
@@ -369,36 +421,24 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
 
   // framebuffer write-back (api/framebuffer.h:93-226) from the primary device, frame by frame.
   // The other ranks of a process gather hold only their tiles: their host pixels are not
-  // written (rank 0's framebuffers receive the gathered frames).
+  // written (rank 0's framebuffers receive the gathered frames). A framebuffer with its own
+  // host pixels keeps a reference to the frame in HBM instead, read back by rtMapFrameBuffer
+  // (the reference's only access to the pixels, singleray_device.cpp:439-447): frames nobody
+  // maps cross no PCIe. YRT_EAGER_READBACK=1: copy at the end of every render.
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  std::vector<float> tmp;
+  static const bool eager = getenv("YRT_EAGER_READBACK") != nullptr;
   for (int k = 0; k < nf && !(procGather && shardIndex != 0); ++k) {
     FrameBufferObj& Fk = *F[k];
-    void* dst = Fk.buffer(Fk.cur);
-    if (Fk.format == FB_RGB8) {
-      HIP_CHECK(hipMemcpy(dst, g0.dFbRGB8.as<uint8_t>() + (size_t)k * rgb8Stride * H, rgb8Stride * H,
-                          hipMemcpyDeviceToHost));
-      continue;
-    }
-    tmp.resize((size_t)W * H * 3);
-    HIP_CHECK(hipMemcpy(tmp.data(), g0.dFbFloat.as<float>() + (size_t)k * W * H * 3, tmp.size() * sizeof(float),
-                        hipMemcpyDeviceToHost));
-    if (Fk.format == FB_RGB_FLOAT32) {
-      memcpy(dst, tmp.data(), tmp.size() * sizeof(float));
-    } else if (Fk.format == FB_RGBA_FLOAT32) {
-      float* o = (float*)dst;
-      for (size_t i = 0; i < (size_t)W * H; ++i) {
-        o[4 * i] = tmp[3 * i]; o[4 * i + 1] = tmp[3 * i + 1]; o[4 * i + 2] = tmp[3 * i + 2]; o[4 * i + 3] = 1.0f;
-      }
-    } else {  // RGBA8: pixel[3] = 0 (framebuffer.h:170-178)
-      uint8_t* o = (uint8_t*)dst;
-      for (size_t i = 0; i < (size_t)W * H; ++i) {
-        for (int c = 0; c < 3; ++c) o[4 * i + c] = (uint8_t)clampf(tmp[3 * i + c] * 255.0f, 0.0f, 255.0f);
-        o[4 * i + 3] = 0;
-      }
-    }
+    FrameBufferObj::Pending pf;
+    pf.keep = g0.blk;
+    pf.src = Fk.format == FB_RGB8 ? (const void*)(g0.fbRGB8() + (size_t)k * rgb8Stride * H)
+                                  : (const void*)(g0.fbFloat() + (size_t)k * W * H * 3);
+    pf.hipDevice = g0.hipDevice;
+    if ((int)Fk.pending.size() < Fk.depth) Fk.pending.resize(Fk.depth);
+    Fk.pending[Fk.cur] = pf;
+    if (eager || !Fk.userPtrs.empty()) fb_read_back(Fk, Fk.cur);
   }
   stats.samples = ctx[0]->stats.samples;
   stats.gather = gatherPath;
@@ -513,11 +553,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   HIP_CHECK(hipMemcpyAsync(g.dCam.p, g.hCams.data(), sizeof(GpuCamera) * nf, hipMemcpyHostToDevice, stream));
   g.dPixelSets.alloc((size_t)W * H);
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  g.dFbFloat.alloc((size_t)nf * W * H * 3 * sizeof(float));
-  g.dFbRGB8.alloc((size_t)nf * rgb8Stride * H);
+  g.blk->fbFloat.alloc((size_t)nf * W * H * 3 * sizeof(float));
+  g.blk->fbRGB8.alloc((size_t)nf * rgb8Stride * H);
   if (count > 1) {  // pixels of other shards stay 0 so per-shard images compose by sum
-    HIP_CHECK(hipMemsetAsync(g.dFbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
-    HIP_CHECK(hipMemsetAsync(g.dFbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));
+    HIP_CHECK(hipMemsetAsync(g.blk->fbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
+    HIP_CHECK(hipMemsetAsync(g.blk->fbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));
   }
 
   FrameView fv;
@@ -548,7 +588,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   const int shardTiles = shard_tiles(numTiles, index, count);
 
   if (R.debug) {
-    launch_debug_render(sv, fv, R.maxDepth, R.spp, numTiles, g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(),
+    launch_debug_render(sv, fv, R.maxDepth, R.spp, numTiles, g.fbFloat(), g.fbRGB8(),
                         (int)rgb8Stride, stream);
   } else {
     launch_pixel_sets(fv, g.dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
@@ -568,7 +608,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
     const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
-    const size_t counterWords = qcounter_index(levels, 0, 0);
+    const size_t counterWords = qcounter_words(levels);
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
@@ -588,6 +628,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipEventRecord(setup, stream));
       for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(g.lanes[l].stream, setup, 0));
     }
+    // shadow rays read their origin from their vertex's continuation record (PathBuffers::sIdx);
+    // YRT_SHADOW_ORG_IDX=0: every shadow ray carries its own origin
+    static const bool shadowOrgIdx = !getenv("YRT_SHADOW_ORG_IDX") || atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
     auto lane_buffers = [&](GpuCtx::Lane& L) {
       PathBuffers pb;
       for (int k = 0; k < 2; ++k) {
@@ -603,6 +646,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.sDir = L.sDir.as<float4>();
       pb.sContrib = L.sContrib.as<float4>();
       pb.sOcc = L.sOcc.as<int>();
+      // the capture frame (roofline accounting) copies whole shadow records: own origins there
+      pb.sIdx = shadowOrgIdx && captureMax == 0 ? L.sIdx.as<int>() : nullptr;
       pb.counters = L.counters.as<unsigned>();
       for (int k = 0; k < 2; ++k) pb.qTime[k] = G.hasMotion ? L.qTime[k].as<float>() : nullptr;
       pb.sTime = G.hasMotion ? L.sTime.as<float>() : nullptr;
@@ -716,9 +761,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         if (numDirect > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {g.ev(), g.ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
-          const ShadowFuse sf{pb.sContrib, pb.pathL};
+          const ShadowFuse sf{pb.fuseShadow ? pb.sContrib : nullptr, pb.pathL, pb.sIdx, pb.qOrg[cur ^ 1]};
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, st, pb.fuseShadow ? &sf : nullptr, hint(estShadow[d]), pb.sTime);
+                           pb.sOcc, st, &sf, hint(estShadow[d]), pb.sTime);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
             g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),
@@ -726,7 +771,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st, hint(estClosest[d]));
         }
       }
-      launch_resolve_pixels(fv, pb, bi, g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), (int)rgb8Stride,
+      launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,
                             g.dAccu.as<float4>(), accumulate ? 1 : 0, st);
       HIP_CHECK(hipMemcpyAsync(L.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       L.pending = true;
@@ -770,7 +815,7 @@ int Device::gather_local(const SlabLayout& base, int numTiles) {
     tiles[k] = shard_tiles(numTiles, lay[k].tileOffset, lay[k].tileStride);
     HIP_CHECK(hipSetDevice(g.hipDevice));
     g.dSlab.alloc((size_t)std::max(1, tiles[k]) * 256 * eb);
-    launch_pack_tiles(g.dFbFloat.as<float>(), g.dFbRGB8.as<uint8_t>(), lay[k], tiles[k], g.dSlab.p, g.stream);
+    launch_pack_tiles(g.fbFloat(), g.fbRGB8(), lay[k], tiles[k], g.dSlab.p, g.stream);
     HIP_CHECK(hipSetDevice(g0.hipDevice));
     g0.recvSlabs[k].alloc((size_t)std::max(1, tiles[k]) * 256 * eb);
   }
@@ -821,7 +866,7 @@ int Device::gather_local(const SlabLayout& base, int numTiles) {
   }
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   for (int k = 1; k < N; ++k)
-    launch_unpack_tiles(g0.recvSlabs[k].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), lay[k], tiles[k],
+    launch_unpack_tiles(g0.recvSlabs[k].p, g0.fbFloat(), g0.fbRGB8(), lay[k], tiles[k],
                         g0.stream);
   try {
     for (int k = 0; k < N; ++k) wait_ctx(k, path == YRT_GATHER_RCCL_LOCAL ? "RCCL slab send/recv" : "slab copy");
@@ -867,7 +912,7 @@ void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) 
     L.tileOffset = shardIndex;
     const int tiles = shard_tiles(numTiles, shardIndex, P);
     g0.dSlab.alloc((size_t)std::max(1, tiles) * 256 * eb);
-    launch_pack_tiles(g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles, g0.dSlab.p, g0.stream);
+    launch_pack_tiles(g0.fbFloat(), g0.fbRGB8(), L, tiles, g0.dSlab.p, g0.stream);
     proc->send_root(g0.dSlab.p, (size_t)tiles * 256 * eb, g0.hipDevice, g0.stream, gatherTimeout);
   } else {
     std::vector<int> tiles(P);
@@ -882,7 +927,7 @@ void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) 
     proc->recv_all(bufs, bytes, g0.hipDevice, g0.stream, gatherTimeout);
     for (int r = 1; r < P; ++r) {
       L.tileOffset = r;
-      launch_unpack_tiles(g0.recvSlabs[r].p, g0.dFbFloat.as<float>(), g0.dFbRGB8.as<uint8_t>(), L, tiles[r],
+      launch_unpack_tiles(g0.recvSlabs[r].p, g0.fbFloat(), g0.fbRGB8(), L, tiles[r],
                           g0.stream);
     }
     HIP_CHECK(hipStreamSynchronize(g0.stream));
@@ -1515,6 +1560,8 @@ void* yrtMapFrameBuffer(YRTDevice dev, YRTHandle fb, int bufID) {
   DEV_GUARD(dev, nullptr)
   auto F = dev->d->get<FrameBufferObj>(fb, "framebuffer");
   const int id = bufID < 0 ? F->cur : bufID;
+  if (id < 0 || id >= F->depth) throw std::runtime_error("rtMapFrameBuffer: invalid buffer id");
+  fb_read_back(*F, id);  // a frame still in HBM comes to the host pixels now
   return F->buffer(id);
   DEV_END(nullptr)
 }

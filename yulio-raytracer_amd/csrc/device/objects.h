@@ -230,6 +230,14 @@ struct FrameBufferObj : Object {
   std::vector<std::unique_ptr<HostPixels>> host;  // one per swapchain buffer (or user pointers)
   std::vector<void*> userPtrs;
   std::vector<float> accu;                 // AccuBuffer (x,y,z,w) per pixel
+  // A frame still on the device (per buffer id): rtRenderFrame leaves it in HBM and
+  // rtMapFrameBuffer copies it to the host pixels on first access (device.cpp fb_read_back).
+  struct Pending {
+    std::shared_ptr<void> keep;  // the device block holding the frame (kept alive until read)
+    const void* src = nullptr;   // RGB8 rows (RGB8 framebuffers) or RGB float32 (the others)
+    int hipDevice = 0;
+  };
+  std::vector<Pending> pending;
   explicit FrameBufferObj(const std::string& t) : Object(Kind::FRAMEBUFFER, t) {}
   void* buffer(int id) { return userPtrs.size() ? userPtrs[id] : host[id]->p; }
 };

@@ -396,6 +396,12 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS_ANY
 #define YRT_NODE_BIAS_ANY 12  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %
 #endif
+#ifndef YRT_SHADE_PAIR_APPEND
+#define YRT_SHADE_PAIR_APPEND 0  // one light: continuation + shadow slots by one 64-bit atomic
+#endif
+#ifndef YRT_NODE_UNROLL_ANY
+#define YRT_NODE_UNROLL_ANY 1  // any-hit: node steps between two node/leaf-phase checks
+#endif
 #ifndef YRT_TRACE_WAVES
 // 6: a scheduling target — the 16 KB LDS stack of a 128-lane block holds the kernels at 5
 // waves/SIMD, but code scheduled for 6 (78/74 VGPRs with SGPR-based node addressing) runs
@@ -545,7 +551,13 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           if (!ANY && q >= 0) YRT_STORE_HIT();
           if (li < end) {
             q = qmap_phys(qm, segCap, li);
-            ro = org[q];
+            if (ANY && sf.orgIdx) {
+              // a shadow ray shares its origin record with its vertex's continuation ray
+              const int oi = sf.orgIdx[q];
+              ro = oi >= 0 ? sf.orgCont[oi] : org[q];
+            } else {
+              ro = org[q];
+            }
             rd = dir[q];
             if (MOTION) rtime = rayTime[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
@@ -609,6 +621,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     if (nNode * 4 > nBlocked * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS)) {
      // consecutive node steps without the retire/refill block in between (+1.5 % on C3)
      while (true) {
+#pragma unroll
+      for (int nu = 0; nu < (ANY ? YRT_NODE_UNROLL_ANY : 1); ++nu) {
       YRT_PROF(2, 1);
       YRT_PROF(3, __popcll(ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
@@ -678,6 +692,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
       }
+      }  // YRT_NODE_UNROLL_ANY
       const int nNode2 = YRT_NNODE();
       const int nBlocked2 = YRT_NBLOCKED();
       if (!(nNode2 * 4 > nBlocked2 * (ANY ? YRT_NODE_BIAS_ANY : YRT_NODE_BIAS))) break;
@@ -1461,26 +1476,19 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       }
     }
     SPROF_MARK(4);  // continuation: CompositedBRDF::sample, Russian roulette
-    bool got;
-    const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
     if (haveL) pb.pathL[path] = make_float4(L.x, L.y, L.z, 0.f);
-    if (got) {
+    // the continuation's records (pathtraceintegrator.cpp:169-213) at queue slot nq
+    auto cont_store = [&](unsigned nq) {
       if (pb.qTime[0]) pb.qTime[cur ^ 1][nq] = samp(fv, 4, rec);  // lastRay.time (:210)
       pb.qPath[cur ^ 1][nq] = path;
       pb.qOrg[cur ^ 1][nq] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
       pb.qDir[cur ^ 1][nq] = make_float4(nwi.x, nwi.y, nwi.z, __int_as_float(0x7f800000));
       pb.qThr[cur ^ 1][nq] = make_float4(nthr.x, nthr.y, nthr.z, __int_as_float(nmeta));
-    }
-    SPROF_MARK(5);  // continuation append and stores
-    SPROF_FINE(2);  // rest of the continuation, append and stores
-
+    };
     // direct lighting: one shadow ray per light (pathtraceintegrator.cpp:123-167); its
     // contribution is added to pathL[path] after the emission above (reference order)
-    for (int k = 0; k < numDirect; ++k) {
+    auto light_term = [&](int k, V3& wi, float& tfar, V3& contrib) -> bool {
       const int li = const_ref(sv.directLights + k);
-      bool pred = false;
-      V3 sOrg = v3s(0.f), wi = v3s(0.f), contrib = v3s(0.f);
-      float tnear = 0.f, tfar = 0.f;
       const YRT_CONST GpuLight& lt = const_ref(sv.lights + li);  // scalar loads
       const bool lit = active && isHit && useDirect && (lt.illumMask & dg.illumMask) != 0;
       V3 Ls = v3s(0.f);
@@ -1509,23 +1517,70 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
         float tMax = rp.tMaxShadowRay + shadowRayJitterLength;
         const float dotProduct = dot(wi, ld3(rp.up));
         if (dotProduct <= 0.f) tMax += rp.tMaxShadowRay * 100.f * smoothstepf(0.f, 1.f, fabsf(dotProduct));
-        sOrg = dg.P;
-        tnear = dg.error * rp.epsilon;
         tfar = tMax - dg.error * rp.epsilon;
         contrib = thr * Ls * brdf * rcpf_(pdf);
-        pred = true;
+        return true;
       }
+      return false;
+    };
+    // shadow ray records at slot si; its origin (dg.P, dg.error * epsilon) is the continuation's
+    // (queue slot nq) when there is one
+    auto shadow_store = [&](unsigned si, const V3& wi, float tfar, const V3& contrib, bool withCont, unsigned nq) {
+      if (pb.sTime) pb.sTime[si] = samp(fv, 4, rec);  // lastRay.time (:158)
+      if (pb.sIdx) pb.sIdx[si] = withCont ? (int)nq : -1;
+      if (!pb.sIdx || !withCont) pb.sOrg[si] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
+      pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
+      pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
+    };
+#if YRT_SHADE_PAIR_APPEND
+    if (numDirect == 1) {
+      // one light: the shadow ray and the continuation take their queue slots with ONE 64-bit
+      // atomic per wave on the segment's counter pair (shadow count of this depth in the low
+      // word, continuation count of the next in the high word, qcounter_index)
+      V3 wi = v3s(0.f), contrib = v3s(0.f);
+      float tfar = 0.f;
+      const bool pred = light_term(0, wi, tfar, contrib);
       SPROF_FINE(5);  // shadow-ray jitter, contribution
-      bool sgot;
-      const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
-      if (sgot) {
-        if (pb.sTime) pb.sTime[si] = samp(fv, 4, rec);  // lastRay.time (:158)
-        pb.sOrg[si] = make_float4(sOrg.x, sOrg.y, sOrg.z, tnear);
-        pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
-        pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
+      const unsigned long long mc = ballot(cont), ms = ballot(pred);
+      unsigned bc = 0, bsh = 0;
+      if (mc | ms) {
+        const int lane = lane_id();
+        const int leader = __ffsll((long long)(mc | ms)) - 1;
+        unsigned long long old = 0;
+        if (lane == leader)
+          old = atomicAdd((unsigned long long*)shadowCount,
+                          (unsigned long long)__popcll(ms) | ((unsigned long long)__popcll(mc) << 32));
+        const unsigned lo = __shfl((unsigned)old, leader, 64), hi = __shfl((unsigned)(old >> 32), leader, 64);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        bsh = lo + (unsigned)__popcll(ms & lt);
+        bc = hi + (unsigned)__popcll(mc & lt);
       }
-      if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numDirect + k] = sgot ? (int)si : -1;
-      SPROF_FINE(6);  // shadow-ray append and stores
+      const unsigned nq = oseg * pb.segCap + bc;
+      const unsigned si = oseg * pb.shSegCap + bsh;
+      if (cont) cont_store(nq);
+      if (pred) shadow_store(si, wi, tfar, contrib, cont, nq);
+      if (active && !pb.fuseShadow) pb.shFirst[q] = pred ? (int)si : -1;
+      SPROF_MARK(5);
+      SPROF_FINE(6);
+    } else
+#endif
+    {
+      bool got;
+      const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
+      if (got) cont_store(nq);
+      SPROF_MARK(5);  // continuation append and stores
+      SPROF_FINE(2);  // rest of the continuation, append and stores
+      for (int k = 0; k < numDirect; ++k) {
+        V3 wi = v3s(0.f), contrib = v3s(0.f);
+        float tfar = 0.f;
+        const bool pred = light_term(k, wi, tfar, contrib);
+        SPROF_FINE(5);  // shadow-ray jitter, contribution
+        bool sgot;
+        const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
+        if (sgot) shadow_store(si, wi, tfar, contrib, got, nq);
+        if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numDirect + k] = sgot ? (int)si : -1;
+        SPROF_FINE(6);  // shadow-ray append and stores
+      }
     }
     SPROF_MARK(6);  // direct light: light sample, BRDF eval, shadow-ray append and stores
 #ifdef YRT_PATH_DEBUG

@@ -71,9 +71,16 @@ struct FrameView {
 #define YRT_QSEGS 32
 #define YRT_QCSTRIDE 64  // unsigned words between two segment counters
 // counters[((level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE], kind 0 = closest queue
-// entering depth `level`, kind 1 = shadow rays emitted at depth `level`.
+// entering depth `level`, kind 1 = shadow rays emitted at depth `level`; except that the
+// closest queue entering depth level > 0 counts in the word after the shadow counter of depth
+// level - 1 (same segment): k_shade appends both with one 64-bit atomic (one light).
 inline __host__ __device__ size_t qcounter_index(int level, int kind, int seg) {
+  if (kind == 0 && level > 0) return ((size_t)((level - 1) * 2 + 1) * YRT_QSEGS + seg) * YRT_QCSTRIDE + 1;
   return ((size_t)(level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE;
+}
+// counter words of a batch of depth levels 0 .. levels - 1
+inline __host__ __device__ size_t qcounter_words(int levels) {
+  return (size_t)(levels * 2) * YRT_QSEGS * YRT_QCSTRIDE;
 }
 inline __host__ __device__ int qseg_capacity(long long items) {
   return (int)(((items + 63) / 64 + YRT_QSEGS - 1) / YRT_QSEGS * 64 + 64);
@@ -91,7 +98,11 @@ struct PathBuffers {
   float4* pathL;     // per path id: radiance so far (emission and unoccluded direct light are
                      // read-modify-written in the reference's order; one writer per path at a time)
   int* shFirst;      // per (queue slot, light): shadow-ray slot or -1
-  float4* sOrg;      // shadow rays
+  float4* sOrg;      // shadow rays (the origin only where sIdx is -1, see sIdx)
+  // per shadow slot: the continuation-queue slot (qOrg[cur ^ 1]) holding the shadow ray's
+  // origin — the same (P, error * epsilon) as the continuation's (pathtraceintegrator.cpp:
+  // 158,210), written once — or -1 (no continuation: the origin is in sOrg). null: sOrg always.
+  int* sIdx;
   float4* sDir;
   float4* sContrib;
   int* sOcc;
@@ -112,6 +123,8 @@ struct PathBuffers {
 struct ShadowFuse {
   const float4* contrib;  // null: not fused, k_trace<true> writes occlusion flags
   float4* pathL;
+  const int* orgIdx;      // PathBuffers::sIdx (null: the origins are the org array's)
+  const float4* orgCont;  // the continuation queue's origins that orgIdx indexes
 };
 
 struct BatchInfo {
