@@ -899,19 +899,27 @@ static void bvh_build_oracle(World* W) {
 typedef struct { V3 org, dir; float tnear, tfar, time; } Ray;
 typedef struct { float t, u, v; int tri; } Hit;
 
+/* the triangle test's cross and dot products with explicit fused multiply-adds, in the order of
+ * the device's tri_cross / tri_dot (kernels/yrt_traverse.h) */
+static inline V3 tri_cross(V3 a, V3 b) {
+  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static inline float tri_dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+
 static inline int tri_test(V3 v0, V3 e1, V3 e2, uint32_t flags, const Ray* r, float tfar, float* t, float* u,
                            float* v) {
-  const V3 Ng = cross(e1, e2);
+  const V3 Ng = tri_cross(e1, e2);
   const V3 C = sub(v0, r->org);
-  const V3 R = cross(r->dir, C);
-  const float den = dot(Ng, r->dir);
+  const V3 R = tri_cross(r->dir, C);
+  const float den = tri_dot(Ng, r->dir);
   const float absDen = fabsf(den);
   const float sgn = den < 0.0f ? -1.0f : 1.0f;
-  const float U = dot(R, e2) * sgn;
-  const float V = dot(R, e1) * sgn;
+  const float U = tri_dot(R, e2) * sgn;
+  const float V = tri_dot(R, e1) * sgn;
   int ok = (den != 0.0f) && (U >= 0.0f) && (V >= 0.0f) && (U + V <= absDen);
   if ((flags & 1u) && !(den > 0.0f)) ok = 0;
-  const float T = dot(Ng, C) * sgn;
+  const float T = tri_dot(Ng, C) * sgn;
   *t = T / absDen;
   ok = ok && (*t > r->tnear) && (*t < tfar);
   *u = U / absDen;
