@@ -288,3 +288,6 @@ def test_bench_two_ranks_cubemap_gather_check(tmp_path):
     assert sc["ranks"] == 2 and sc["n_gpus"] == 1
     assert sc["gather_check"] == "bit_exact", sc
     assert sc["single_gpu_ms_per_cubemap"] > 0
+    # several cubemaps by default at N > 1, reported as median and min per cubemap
+    assert sc["frames"] == 6 and 0 < sc["ms_per_cubemap_min"] <= sc["ms_per_cubemap_median"]
+    assert "note" in line["roofline"]["kernel_ms_per_step"]

@@ -15,6 +15,7 @@ so = Path("/tmp/b8v.so")
 subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", str(so), str(ROOT / "tools" / "bvh8_visits_exp.c"), "-lm"],
                check=True)
 lib = C.CDLL(str(so))
+lib.bvh8_visits.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
 d = np.load(sys.argv[1] if len(sys.argv) > 1 else ROOT / "gpurun_out" / "shadow_c3.npz")
 nodes, tris = np.ascontiguousarray(d["nodes"]), np.ascontiguousarray(d["tris"])
 for depth in range(3):
