@@ -140,6 +140,7 @@ int bvh8_visits(const N4* nodes, int numNodes, const Tri* tris, const float* org
           /* farthest to slot 0 by the kernel's comparator networks */
 #define SW(a, b) do { if (t[b] > t[a]) { float x = t[a]; t[a] = t[b]; t[b] = x; int y = c[a]; c[a] = c[b]; c[b] = y; } } while (0)
           if (w) { SW(0, 1); SW(2, 3); SW(4, 5); SW(6, 7); SW(0, 2); SW(4, 6); SW(0, 4); }
+          else if (getenv("B8V_FULLSORT")) { SW(0, 1); SW(2, 3); SW(0, 2); SW(1, 3); SW(1, 2); }
           else { SW(0, 1); SW(2, 3); SW(0, 2); }
 #undef SW
           for (int j = k - 1; j >= 1; --j)

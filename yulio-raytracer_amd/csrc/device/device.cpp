@@ -681,7 +681,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     };
     std::vector<int64_t> curTiles(nf);
     std::vector<long long> estClosest(levels, -1), estShadow(levels, -1);
-    auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + 65536; };
+    // a launch's grid covers 1.5x the estimate plus a pad (the kernels grid-stride over the
+    // device-side count, so a short estimate costs time, never correctness); YRT_HINT_PAD
+    static const long long hintPad = getenv("YRT_HINT_PAD") ? atoll(getenv("YRT_HINT_PAD")) : 65536;
+    auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + hintPad; };
     // waits for the lane's previous batch and accounts its queue counters
     int64_t tilesDone = 0;
     auto drain = [&](GpuCtx::Lane& L) {
