@@ -234,10 +234,12 @@ __device__ void camera_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir,
   const V3 rvx = v3(R[3] + R[4] * cs, R[9] * omc + R[2] * sn, R[10] * omc - R[1] * sn);
   const V3 rvy = v3(R[9] * omc - R[2] * sn, R[5] + R[6] * cs, R[11] * omc + R[0] * sn);
   const V3 rvz = v3(R[10] * omc + R[1] * sn, R[11] * omc - R[0] * sn, R[7] + R[8] * cs);
-  const V3 bp = (cam.negO[0] * rvx + cam.negO[1] * rvy + cam.negO[2] * rvz) + ld3(cam.rotP);
+  // the rotation's products through the fused LinearSpace3 * v helper, as the oracle's lmul
+  const L3 rot = l3(rvx, rvy, rvz);
+  const V3 bp = mul(rot, ld3(cam.negO)) + ld3(cam.rotP);
   const auto* z = cam.zero[eyeCubeFaceIndex];
   const V3 eye = v3(eyeOffset * p2w.l.vx.x + z[0], eyeOffset * p2w.l.vx.y + z[1], eyeOffset * p2w.l.vx.z + z[2]) + p2w.p;
-  org = (eye.x * rvx + eye.y * rvy + eye.z * rvz) + bp;
+  org = mul(rot, eye) + bp;
   const auto* m = cam.lin[eyeCubeFaceIndex];
   dir = normalize(fx * v3(m[0], m[1], m[2]) + yPixel * v3(m[3], m[4], m[5]) + v3(m[6], m[7], m[8]));
 }
