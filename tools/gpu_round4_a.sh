@@ -4,7 +4,9 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_r4a.log 2>&1; rc=$?; tail -n 3 gpurun_out/pytest_r4a.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 480 python -u -m pytest tests -m gpu -q --maxfail=12 --timeout 200 --timeout-method thread > gpurun_out/pytest_r4a.log 2>&1; rc=$?; grep -E "^FAILED|passed|failed" gpurun_out/pytest_r4a.log | tail -n 14
+# parity failures (rc 1) still leave the measurements below meaningful; anything else ends the batch
+[ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r4a.log 2>&1 || exit $?
 tail -n 1 gpurun_out/smoke_r4a.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_r4a.json 2> gpurun_out/bench_r4a.err || exit $?

@@ -628,9 +628,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipEventRecord(setup, stream));
       for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(g.lanes[l].stream, setup, 0));
     }
-    // shadow rays read their origin from their vertex's continuation record (PathBuffers::sIdx);
-    // YRT_SHADOW_ORG_IDX=0: every shadow ray carries its own origin
-    static const bool shadowOrgIdx = !getenv("YRT_SHADOW_ORG_IDX") || atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
+    // YRT_SHADOW_ORG_IDX=1: shadow rays read their origin from their vertex's continuation
+    // record (PathBuffers::sIdx) instead of carrying their own. Off: k_shade -2 % but the
+    // any-hit kernel's dependent origin load +2.5 %, frame -0.3 % (profiles/r04/ab_r04a.txt)
+    static const bool shadowOrgIdx = getenv("YRT_SHADOW_ORG_IDX") && atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
     auto lane_buffers = [&](GpuCtx::Lane& L) {
       PathBuffers pb;
       for (int k = 0; k < 2; ++k) {

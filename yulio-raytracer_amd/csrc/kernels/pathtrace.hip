@@ -399,7 +399,9 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_NODE_BIAS_ANY 12  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %
 #endif
 #ifndef YRT_SHADE_PAIR_APPEND
-#define YRT_SHADE_PAIR_APPEND 0  // one light: continuation + shadow slots by one 64-bit atomic
+// one light: continuation + shadow slots by one 64-bit atomic per wave instead of two 32-bit
+// ones (same box: k_shade -2.2 %, frame +0.5 %, profiles/r04/ab_r04a.txt)
+#define YRT_SHADE_PAIR_APPEND 1
 #endif
 #ifndef YRT_NODE_UNROLL_ANY
 #define YRT_NODE_UNROLL_ANY 1  // any-hit: node steps between two node/leaf-phase checks

@@ -147,13 +147,16 @@ _sig(dev, "yrtSetTileShard", i32, vp, i32, i32)
 _sig(dev, "yrtShardCommUniqueId", i32, vp)
 _sig(dev, "yrtSetShardComm", i32, vp, i32, i32, vp)
 _sig(dev, "yrtRcclAvailable", i32)
-_sig(dev, "yrtNewShardHub", vp, i32)
-_sig(dev, "yrtDeleteShardHub", None, vp)
-_sig(dev, "yrtSetShardHub", i32, vp, vp, i32)
-_sig(dev, "yrtSetGatherTimeout", i32, vp, C.c_double)
-_sig(dev, "yrtShardHubStatus", i32, vp, i32, i32, C.c_double)
-_sig(dev, "yrtShardHubSlab", i32, vp, i32, vp, sz, vp, sz, C.c_double)
-_sig(dev, "yrtShardHubLastError", cstr)
+try:  # absent from builds before round 4 selected with YRT_LIB_DIR (same-box A/B variants)
+    _sig(dev, "yrtNewShardHub", vp, i32)
+    _sig(dev, "yrtDeleteShardHub", None, vp)
+    _sig(dev, "yrtSetShardHub", i32, vp, vp, i32)
+    _sig(dev, "yrtSetGatherTimeout", i32, vp, C.c_double)
+    _sig(dev, "yrtShardHubStatus", i32, vp, i32, i32, C.c_double)
+    _sig(dev, "yrtShardHubSlab", i32, vp, i32, vp, sz, vp, sz, C.c_double)
+    _sig(dev, "yrtShardHubLastError", cstr)
+except AttributeError:
+    pass
 _sig(dev, "yrtGetDeviceCount", i32, vp)
 _sig(dev, "yrtSetRefitCommits", i32, vp, i32)
 _sig(dev, "yrtGetSceneRefits", i32, vp, vp)
