@@ -908,13 +908,12 @@ static void bvh_build_oracle(World* W) {
 typedef struct { V3 org, dir; float tnear, tfar, time; } Ray;
 typedef struct { float t, u, v; int tri; } Hit;
 
-/* the triangle test's cross and dot products with explicit fused multiply-adds, in the order of
- * the device's tri_cross / tri_dot (kernels/yrt_traverse.h) */
+/* the triangle test's cross and dot products as separate multiplies and adds (two roundings per
+ * term pair), in the order of the device's tri_cross / tri_dot (kernels/yrt_traverse.h) */
 static inline V3 tri_cross(V3 a, V3 b) {
-  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
-            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-static inline float tri_dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+static inline float tri_dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
 static inline int tri_test(V3 v0, V3 e1, V3 e2, uint32_t flags, const Ray* r, float tfar, float* t, float* u,
                            float* v) {

@@ -271,13 +271,23 @@ def test_tile_shards_compose_bit_exact(gpu_device):
     s = yrt.Session(args, device=gpu_device)
     full = s.render()
     parts = []
-    for k in range(3):
-        gpu_device.set_tile_shard(k, 3)
-        parts.append(s.render())
-    gpu_device.set_tile_shard(0, 1)
+    try:
+        for k in range(3):
+            gpu_device.set_tile_shard(k, 3)
+            parts.append(s.render())
+            # the same shard again: its frame block already holds the zeros outside the shard
+            # and is not cleared again (device.cpp FrameBlock::zeroKey)
+            assert np.array_equal(s.render(), parts[-1])
+        gpu_device.set_tile_shard(0, 1)
+        assert np.array_equal(s.render(), full)
+        gpu_device.set_tile_shard(1, 3)  # after a whole frame the block is cleared again
+        again = s.render()
+    finally:
+        gpu_device.set_tile_shard(0, 1)
     from yrt.dist import tile_mask
     for k, p in enumerate(parts):
         assert not p[~tile_mask(200, 200, k, 3)].any()
+    assert np.array_equal(again, parts[1])
     assert np.array_equal(sum(parts), full)
     s.close()
 

@@ -13,8 +13,9 @@ is the slowest share; efficiency = T(1) / (N * T(N)).
 
 --mode face: one rtRenderFrame per face (the reference's loop);
 --mode cube: the 12 faces in one yrtRenderFrames call (tiles of all faces in one sequence).
-Times are render-only: each call writes its frames back into the session's host framebuffers
-(as the product does) but the images are not converted to numpy arrays.
+Times are render-only: the frames stay in HBM until mapped (as the product does) and are not
+converted to numpy arrays. Each rank's share is rendered twice untimed first: the steady state of
+an N-GPU run, where a rank renders the same share every frame.
 
 usage: python tools/cube_shard_time.py C4|C5 [--mode face|cube] [--gpus 1,2,4,8] [--ranks all|0]
        [--spp N] [--size S]
@@ -95,6 +96,12 @@ def main():
             render_cube(ses, a.cfg, a.mode)
         for r in ranks:
             dev.set_tile_shard(r, n)
+            if n > 1:
+                # untimed: a rank of an N-GPU run renders the same share every frame, so its
+                # two frame blocks (render k+1 writes the block render k's unread frames do
+                # not hold) already hold zeros outside the share (device.cpp FrameBlock::zeroKey)
+                for _ in range(2):
+                    render_cube(ses, a.cfg, a.mode)
             t = time.perf_counter()
             rays += render_cube(ses, a.cfg, a.mode)
             times[r] = time.perf_counter() - t

@@ -55,11 +55,21 @@ struct GpuCtx {
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, sIdx, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
     int64_t pathCap = 0, shadowCap = 0;
-    unsigned* hc = nullptr;  // pinned copy of the counters of the lane's last batch
-    size_t hcWords = 0;
-    bool pending = false;    // a batch was enqueued whose counters are not yet accounted
-    int64_t pendTiles = 0;   // tiles done once that batch drains (progress)
-    std::vector<int64_t> pendFrameTiles;  // that batch's tiles per frame (grid-size hints)
+    // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
+    // copy of the counters (written by the stream after the batch's last trace), the event
+    // after that copy, the batch's tiles (progress) and its tiles per frame (grid-size hints).
+    // The host enqueues up to kPendDepth batches per lane ahead of the GPU, so the next batch's
+    // launches are queued before the lane finishes the previous one.
+    struct Pend {
+      unsigned* hc = nullptr;
+      size_t hcWords = 0;
+      hipEvent_t done = nullptr;
+      int64_t tiles = 0;
+      std::vector<int64_t> frameTiles;
+    };
+    static constexpr int kPendDepth = 2;
+    Pend pend[kPendDepth];
+    int pendHead = 0, pendCount = 0;
   };
   static constexpr int kMaxLanes = 4;      // YRT_LANES may ask for up to 4 (the sweeps of DESIGN §3)
   static constexpr int kDefaultLanes = 2;  // two: C3 +4 % over one, three or four no better
@@ -71,6 +81,9 @@ struct GpuCtx {
   // them back, so the next job renders into the spare (or a fresh) block meanwhile.
   struct FrameBlock {
     DevBuf fbFloat, fbRGB8;
+    // the shard layout (index, count, width, height, frames) whose other shards' pixels this
+    // block holds as zeros (a one-shard render writes only its own tiles); -1: unknown
+    long long zeroKey[5] = {-1, -1, -1, -1, -1};
   };
   std::shared_ptr<FrameBlock> blk = std::make_shared<FrameBlock>(), spareBlk;
   float* fbFloat() const { return blk->fbFloat.as<float>(); }
@@ -79,6 +92,9 @@ struct GpuCtx {
   std::vector<GpuCamera> hCams;  // the job's cameras, one per frame (uploaded to dCam)
   DevBuf dBackplate;                       // the renderer's backplate image (texels)
   uint64_t backplateSerial = 0;            // ImageObj::serial of the image dBackplate holds
+  // (width, height, sets) of the pixel-set map dPixelSets holds: the map depends on nothing else
+  // (integratorrenderer.cpp:126-131 seeds by tile position), so a frame of the same size reuses it
+  long long pixelSetsKey[3] = {-1, -1, -1};
   std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
@@ -99,7 +115,10 @@ struct GpuCtx {
     (void)hipSetDevice(hipDevice);
     for (auto e : eventPool) (void)hipEventDestroy(e);
     for (Lane& L : lanes) {
-      if (L.hc) (void)hipHostFree(L.hc);
+      for (Lane::Pend& P : L.pend) {
+        if (P.hc) (void)hipHostFree(P.hc);
+        if (P.done) (void)hipEventDestroy(P.done);
+      }
       if (L.stream) (void)hipStreamDestroy(L.stream);
     }
   }
@@ -134,7 +153,7 @@ struct GpuCtx {
       L.sDir.alloc(S * 16);
       L.sContrib.alloc(S * 16);
       L.sOcc.alloc(S * 4);
-      L.sIdx.alloc(S * 4);
+      if (shadow_origin_index_built()) L.sIdx.alloc(S * 4);
       L.shadowCap = S;
     }
     if (motion) {
@@ -273,6 +292,9 @@ class Device {
   void render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vector<CameraObj*>& C, ToneMapperObj& T,
                     int W, int H, int index, int count, int accumulate, bool reportProgress);
   int gather_local(const SlabLayout& base, int numTiles);
+  // the render's output is this shard alone (no gather fills the other shards' tiles): those
+  // pixels must read as zeros, so per-shard images compose by sum
+  bool shardZero = true;
   void gather_process(const SlabLayout& base, int numTiles, bool localOk);
   // a process gather is armed: every render of this device joins the ranks' status exchange
   bool proc_gather_armed() const {
@@ -378,6 +400,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     }
     std::vector<GpuScene*> scenes(nr);
     for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
+    shardZero = nr == 1 && !procGather;
     if (nr == 1) {
       render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
     } else {
@@ -553,11 +576,23 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   HIP_CHECK(hipMemcpyAsync(g.dCam.p, g.hCams.data(), sizeof(GpuCamera) * nf, hipMemcpyHostToDevice, stream));
   g.dPixelSets.alloc((size_t)W * H);
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  g.blk->fbFloat.alloc((size_t)nf * W * H * 3 * sizeof(float));
-  g.blk->fbRGB8.alloc((size_t)nf * rgb8Stride * H);
-  if (count > 1) {  // pixels of other shards stay 0 so per-shard images compose by sum
-    HIP_CHECK(hipMemsetAsync(g.blk->fbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
-    HIP_CHECK(hipMemsetAsync(g.blk->fbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));
+  GpuCtx::FrameBlock& B = *g.blk;
+  const void* const oldF = B.fbFloat.p;
+  const void* const oldB = B.fbRGB8.p;
+  B.fbFloat.alloc((size_t)nf * W * H * 3 * sizeof(float));
+  B.fbRGB8.alloc((size_t)nf * rgb8Stride * H);
+  const long long zkey[5] = {index, count, W, H, nf};
+  if (B.fbFloat.p != oldF || B.fbRGB8.p != oldB) B.zeroKey[0] = -1;
+  if (count > 1 && shardZero && !R.debug) {
+    // pixels of other shards stay 0 so per-shard images compose by sum; a block that already
+    // holds this layout's zeros (the same shard rendered into it before) is not cleared again
+    if (memcmp(B.zeroKey, zkey, sizeof(zkey)) != 0) {
+      HIP_CHECK(hipMemsetAsync(B.fbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
+      HIP_CHECK(hipMemsetAsync(B.fbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));
+      memcpy(B.zeroKey, zkey, sizeof(zkey));
+    }
+  } else {
+    B.zeroKey[0] = -1;  // every tile gets written (one shard, the gather, the debug renderer)
   }
 
   FrameView fv;
@@ -591,7 +626,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     launch_debug_render(sv, fv, R.maxDepth, R.spp, numTiles, g.fbFloat(), g.fbRGB8(),
                         (int)rgb8Stride, stream);
   } else {
-    launch_pixel_sets(fv, g.dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
+    if (g.pixelSetsKey[0] != W || g.pixelSetsKey[1] != H || g.pixelSetsKey[2] != rp.sets) {
+      launch_pixel_sets(fv, g.dPixelSets.as<uint8_t>(), W, H, rp.sets, stream);
+      g.pixelSetsKey[0] = W;
+      g.pixelSetsKey[1] = H;
+      g.pixelSetsKey[2] = rp.sets;
+    }
     g.capClosest.clear();
     g.capShadow.clear();
     const int spp = rp.spp;
@@ -615,23 +655,35 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), numDirect, G.hasMotion);
       L.counters.alloc(counterWords * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
-      if (L.hcWords < counterWords) {
-        if (L.hc) HIP_CHECK(hipHostFree(L.hc));
-        HIP_CHECK(hipHostMalloc((void**)&L.hc, counterWords * sizeof(unsigned), hipHostMallocDefault));
-        L.hcWords = counterWords;
+      for (GpuCtx::Lane::Pend& Pd : L.pend) {
+        if (Pd.hcWords < counterWords) {
+          if (Pd.hc) HIP_CHECK(hipHostFree(Pd.hc));
+          Pd.hc = nullptr;
+          Pd.hcWords = 0;
+          HIP_CHECK(hipHostMalloc((void**)&Pd.hc, counterWords * sizeof(unsigned), hipHostMallocDefault));
+          Pd.hcWords = counterWords;
+        }
+        if (!Pd.done) HIP_CHECK(hipEventCreateWithFlags(&Pd.done, hipEventDisableTiming));
       }
-      L.pending = false;
+      L.pendHead = L.pendCount = 0;
     }
+    // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH: 1 = wait for the
+    // lane's previous batch before enqueueing the next)
+    static const int pendDepth =
+        std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH"))
+                                                                                 : GpuCtx::Lane::kPendDepth));
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
     if (nl > 1) {
       hipEvent_t setup = g.ev();
       HIP_CHECK(hipEventRecord(setup, stream));
       for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(g.lanes[l].stream, setup, 0));
     }
-    // YRT_SHADOW_ORG_IDX=1: shadow rays read their origin from their vertex's continuation
-    // record (PathBuffers::sIdx) instead of carrying their own. Off: k_shade -2 % but the
-    // any-hit kernel's dependent origin load +2.5 %, frame -0.3 % (profiles/r04/ab_r04a.txt)
-    static const bool shadowOrgIdx = getenv("YRT_SHADOW_ORG_IDX") && atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
+    // YRT_SHADOW_ORG_IDX=1 (kernels built with -DYRT_SHADOW_ORG_IDX=1): shadow rays read their
+    // origin from their vertex's continuation record (PathBuffers::sIdx) instead of carrying
+    // their own. Off: k_shade -2 % but the any-hit kernel's dependent origin load +2.5 %,
+    // frame -0.3 % (profiles/r04/ab_r04a.txt)
+    static const bool shadowOrgIdx =
+        shadow_origin_index_built() && getenv("YRT_SHADOW_ORG_IDX") && atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
     auto lane_buffers = [&](GpuCtx::Lane& L) {
       PathBuffers pb;
       for (int k = 0; k < 2; ++k) {
@@ -686,22 +738,30 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // device-side count, so a short estimate costs time, never correctness); YRT_HINT_PAD
     static const long long hintPad = getenv("YRT_HINT_PAD") ? atoll(getenv("YRT_HINT_PAD")) : 65536;
     auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + hintPad; };
-    // waits for the lane's previous batch and accounts its queue counters
+    // accounts the queue counters of the lane's oldest pending batch; without `wait` only if
+    // the batch's counters have arrived (returns whether it accounted one)
     int64_t tilesDone = 0;
-    auto drain = [&](GpuCtx::Lane& L) {
-      if (!L.pending) return;
-      HIP_CHECK(hipStreamSynchronize(L.stream));
+    auto drain_one = [&](GpuCtx::Lane& L, bool wait) -> bool {
+      if (L.pendCount == 0) return false;
+      GpuCtx::Lane::Pend& Pd = L.pend[L.pendHead];
+      if (wait) {
+        HIP_CHECK(hipEventSynchronize(Pd.done));
+      } else {
+        const hipError_t q = hipEventQuery(Pd.done);
+        if (q == hipErrorNotReady) return false;
+        HIP_CHECK(q);
+      }
       for (int d = 0; d < levels; ++d) {
         double nc = 0, ns = 0;
         for (int k = 0; k < YRT_QSEGS; ++k) {
-          nc += L.hc[qcounter_index(d, 0, k)];
-          ns += L.hc[qcounter_index(d, 1, k)];
+          nc += Pd.hc[qcounter_index(d, 0, k)];
+          ns += Pd.hc[qcounter_index(d, 1, k)];
         }
         // the batch's rate per tile, credited to each of its frames
         for (int f = 0; f < nf; ++f)
-          if (L.pendFrameTiles[f]) {
-            rateC[(size_t)f * levels + d] = nc / (double)L.pendTiles;
-            rateS[(size_t)f * levels + d] = ns / (double)L.pendTiles;
+          if (Pd.frameTiles[f]) {
+            rateC[(size_t)f * levels + d] = nc / (double)Pd.tiles;
+            rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
           }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           g.stats.raysClosest += nc;
@@ -710,9 +770,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         g.stats.raysShadow += ns;
         if (d < rp.maxDepth && ns) g.stats.launchesShadow += 1;
       }
-      L.pending = false;
-      tilesDone += L.pendTiles;
+      L.pendHead = (L.pendHead + 1) % GpuCtx::Lane::kPendDepth;
+      L.pendCount -= 1;
+      tilesDone += Pd.tiles;
       if (reportProgress) status(R, 1, float(tilesDone) / float(std::max(1, shardTiles)));
+      return true;
     };
 
     struct EvPair { hipEvent_t a, b; int kind; };
@@ -721,7 +783,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
       if (R.stopFlag && R.stopFlag->load()) break;
       GpuCtx::Lane& L = g.lanes[batch % nl];
-      drain(L);
+      // account the batches that have finished, then make room in this lane's ring
+      for (int l = 0; l < nl; ++l)
+        while (drain_one(g.lanes[l], false)) {}
+      while (L.pendCount >= pendDepth) drain_one(L, true);
       const hipStream_t st = L.stream;
       const PathBuffers pb = lane_buffers(L);
       SceneView lsv = sv;
@@ -775,14 +840,19 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st, hint(estClosest[d]));
         }
       }
+      // the counters are final after the last trace: their copy runs before the pixel resolve,
+      // so the host learns the batch's queue sizes while the resolve still runs
+      GpuCtx::Lane::Pend& Pd = L.pend[(L.pendHead + L.pendCount) % GpuCtx::Lane::kPendDepth];
+      HIP_CHECK(hipMemcpyAsync(Pd.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipEventRecord(Pd.done, st));
+      Pd.tiles = bi.numPixels / 256;
+      Pd.frameTiles.assign(curTiles.begin(), curTiles.end());
+      L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,
                             g.dAccu.as<float4>(), accumulate ? 1 : 0, st);
-      HIP_CHECK(hipMemcpyAsync(L.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-      L.pending = true;
-      L.pendTiles = bi.numPixels / 256;
-      L.pendFrameTiles.assign(curTiles.begin(), curTiles.end());
     }
-    for (int l = 0; l < nl; ++l) drain(g.lanes[l]);
+    for (int l = 0; l < nl; ++l)
+      while (drain_one(g.lanes[l], true)) {}
     for (auto& e : evs) {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));

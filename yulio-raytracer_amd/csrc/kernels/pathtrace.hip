@@ -398,10 +398,20 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS_ANY
 #define YRT_NODE_BIAS_ANY 12  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %
 #endif
+#ifndef YRT_SHADOW_ORG_IDX
+// 1: a shadow ray may read its origin from its vertex's continuation record (PathBuffers::sIdx,
+// enabled at run time by YRT_SHADOW_ORG_IDX=1). Compiled out by default: k_shade -2 % but the
+// any-hit refill's dependent origin load +2.5 %, frame -0.3 % (profiles/r04/ab_r04a.txt), and
+// the runtime branch held registers in both kernels (k_shade scratch spills on C4)
+#define YRT_SHADOW_ORG_IDX 0
+#endif
 #ifndef YRT_SHADE_PAIR_APPEND
-// one light: continuation + shadow slots by one 64-bit atomic per wave instead of two 32-bit
-// ones (same box: k_shade -2.2 %, frame +0.5 %, profiles/r04/ab_r04a.txt)
-#define YRT_SHADE_PAIR_APPEND 1
+// 1: with one light, the continuation and shadow slots by one 64-bit atomic per wave instead of
+// two 32-bit ones. Off: C3 k_shade -2.2 % but frame +0.3 % within the spread
+// (profiles/r04/ab_r04a.txt), and the light term then runs with the continuation's records
+// live: C4's MetallicPaint kernel spills 37 VGPRs to scratch and its cubemap runs 4.5 % slower
+// (profiles/r04/bisect_r04.txt)
+#define YRT_SHADE_PAIR_APPEND 0
 #endif
 #ifndef YRT_NODE_UNROLL_ANY
 #define YRT_NODE_UNROLL_ANY 1  // any-hit: node steps between two node/leaf-phase checks
@@ -555,6 +565,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           if (!ANY && q >= 0) YRT_STORE_HIT();
           if (li < end) {
             q = qmap_phys(qm, segCap, li);
+#if YRT_SHADOW_ORG_IDX
             if (ANY && sf.orgIdx) {
               // a shadow ray shares its origin record with its vertex's continuation ray
               const int oi = sf.orgIdx[q];
@@ -562,6 +573,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             } else {
               ro = org[q];
             }
+#else
+            ro = org[q];
+#endif
             rd = dir[q];
             if (MOTION) rtime = rayTime[q];
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
@@ -1531,8 +1545,14 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     // (queue slot nq) when there is one
     auto shadow_store = [&](unsigned si, const V3& wi, float tfar, const V3& contrib, bool withCont, unsigned nq) {
       if (pb.sTime) pb.sTime[si] = samp(fv, 4, rec);  // lastRay.time (:158)
+#if YRT_SHADOW_ORG_IDX
       if (pb.sIdx) pb.sIdx[si] = withCont ? (int)nq : -1;
       if (!pb.sIdx || !withCont) pb.sOrg[si] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
+#else
+      (void)withCont;
+      (void)nq;
+      pb.sOrg[si] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
+#endif
       pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
       pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
     };
@@ -1794,6 +1814,8 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
     hipLaunchKernelGGL((k_trace<false, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
                        segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr);
 }
+
+bool shadow_origin_index_built() { return YRT_SHADOW_ORG_IDX != 0; }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, long long countHint,

@@ -146,6 +146,8 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
                           int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1,
                           const float* time = nullptr);
+// whether the kernels were built with the shared shadow-ray origins (-DYRT_SHADOW_ORG_IDX=1)
+bool shadow_origin_index_built();
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr,
                       long long countHint = -1, const float* time = nullptr);

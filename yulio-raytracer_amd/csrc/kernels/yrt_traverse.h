@@ -6,7 +6,7 @@
 // Hit convention (restated from the in-tree copy lights/trianglelight.h:55-65 and the
 // rtcore triangle layout; Embree itself is binary-only so this is "parity unpinned"
 // against Embree and pinned against oracle/):
-//   e1 = v0-v1, e2 = v2-v0, Ng = cross(e1,e2), C = v0-O, R = cross(D,C)  (fused, tri_cross)
+//   e1 = v0-v1, e2 = v2-v0, Ng = cross(e1,e2), C = v0-O, R = cross(D,C)  (tri_cross)
 //   den = dot(Ng,D), U = dot(R,e2)*sgn(den), V = dot(R,e1)*sgn(den), T = dot(Ng,C)*sgn(den)
 //   valid: den != 0, U >= 0, V >= 0, U+V <= |den|, tnear < t=T/|den| < tfar
 //   back-face filter (cullBackFaces meshes, shapes/trianglemesh_full.cpp:86-106): reject den <= 0
@@ -319,16 +319,14 @@ __device__ __forceinline__ void sort3_far(float t[4], int c[4]) {
 #undef YRT_CSWAP_D
 }
 
-// The triangle test's cross and dot products with explicit fused multiply-adds (one rounding per
-// term pair: 27 instead of 43 VALU per test); the oracle's tri_cross / tri_dot evaluate the same
-// operations (oracle/yrt_oracle.c), so hits stay bit-identical.
+// The triangle test's cross and dot products as separate multiplies and adds (two roundings per
+// term pair, -ffp-contract=off), the oracle's tri_cross / tri_dot (oracle/yrt_oracle.c). An
+// explicit-FMA form issues 27 instead of 43 VALU per test but ran the closest-hit trace 2 %
+// slower on C3 and the C4 cubemap 2 % slower (same-box bisect, profiles/r04/bisect_r04.txt).
 __device__ __forceinline__ V3 tri_cross(const V3& a, const V3& b) {
-  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
-            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-__device__ __forceinline__ float tri_dot(const V3& a, const V3& b) {
-  return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
-}
+__device__ __forceinline__ float tri_dot(const V3& a, const V3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
 // One triangle without the distance range: true when the ray's line crosses the triangle
 // (barycentric and back-face tests); t, U, V, absDen as tri_test_t.
