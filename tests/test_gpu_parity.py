@@ -292,13 +292,24 @@ def test_tile_shards_compose_bit_exact(gpu_device):
     s.close()
 
 
-def test_batch_capacity_invariance(gpu_device):
+def test_batch_capacity_invariance(gpu_device, monkeypatch):
     s = _session(gpu_device, c2_args(160, 4))
     a = s.render()
     gpu_device.set_batch_capacity(256 * 4 * 3)  # 3 tiles per wavefront batch (34 batches, both lanes)
-    b = s.render()
-    gpu_device.set_batch_capacity(64 << 20)
+    try:
+        b = s.render()
+        # the lanes' batch rings one deep (wait for a lane's previous batch before the next), and
+        # the last round of batches cut in half-size batches
+        monkeypatch.setenv("YRT_PEND_DEPTH", "1")
+        c = s.render()
+        monkeypatch.delenv("YRT_PEND_DEPTH")
+        monkeypatch.setenv("YRT_TAPER", "1")
+        d = s.render()
+    finally:
+        gpu_device.set_batch_capacity(64 << 20)
     assert np.array_equal(a, b)
+    assert np.array_equal(a, c)
+    assert np.array_equal(a, d)
     s.close()
 
 

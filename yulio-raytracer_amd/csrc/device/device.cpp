@@ -669,7 +669,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     }
     // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH: 1 = wait for the
     // lane's previous batch before enqueueing the next)
-    static const int pendDepth =
+    const int pendDepth =
         std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH"))
                                                                                  : GpuCtx::Lane::kPendDepth));
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
@@ -780,7 +780,21 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     struct EvPair { hipEvent_t a, b; int kind; };
     std::vector<EvPair> evs;
     int64_t batch = 0;
-    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
+    // batch boundaries (first tile of each batch, then shardTiles). YRT_TAPER=1: the last round of
+    // batches (one per lane) is cut into twice as many half batches, so the lanes' final depth
+    // tails are shorter and end closer together
+    std::vector<int64_t> bounds;
+    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch) bounds.push_back(first);
+    const bool taper = getenv("YRT_TAPER") && atoi(getenv("YRT_TAPER")) != 0;
+    if (taper && nl > 1 && (int64_t)bounds.size() >= 2 * nl) {
+      const int64_t lastRound = bounds[bounds.size() - nl];
+      bounds.resize(bounds.size() - nl);
+      const int64_t rest = shardTiles - lastRound, pieces = 2 * nl, per = (rest + pieces - 1) / pieces;
+      for (int64_t f = lastRound; f < shardTiles; f += per) bounds.push_back(f);
+    }
+    bounds.push_back(shardTiles);
+    for (size_t bix = 0; bix + 1 < bounds.size(); ++bix, ++batch) {
+      const int64_t first = bounds[bix], batchTiles = bounds[bix + 1] - first;
       if (R.stopFlag && R.stopFlag->load()) break;
       GpuCtx::Lane& L = g.lanes[batch % nl];
       // account the batches that have finished, then make room in this lane's ring
@@ -793,7 +807,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       lsv.traceSpill = L.spill.as<int>();
       BatchInfo bi;
       bi.firstTile = (int)first;
-      bi.numPixels = (int)(std::min<int64_t>(tilesPerBatch, shardTiles - first) * 256);
+      bi.numPixels = (int)(batchTiles * 256);
       bi.tileStride = count;
       bi.tileOffset = index;
       bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
