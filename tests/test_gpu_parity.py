@@ -313,6 +313,32 @@ def test_batch_capacity_invariance(gpu_device, monkeypatch):
     s.close()
 
 
+@pytest.mark.parametrize("which", ["C3", "C4"])
+def test_fused_primary_invariance(gpu_device, monkeypatch, which):
+    """Depth 0 as one kernel (camera rays generated and misses resolved inside the closest-hit
+    trace, launch_trace_primary) against k_raygen + the queued trace: bit-identical frames and
+    the same query counts; C3's dome and C4's zero HDRI both take the fused path."""
+    out = []
+    for prim in ("0", "1"):
+        monkeypatch.setenv("YRT_PRIMARY", prim)
+        gpu_device.set_batch_capacity(256 * 16 * 5)  # several batches on both lanes
+        try:
+            if which == "C3":
+                s = _session(gpu_device, c3_args(96, 4))
+                img = [s.render()]
+            else:
+                s = _session(gpu_device, c4_args(64, 2))
+                img = s.render_cube()
+            st = gpu_device.render_stats()
+        finally:
+            gpu_device.set_batch_capacity(64 << 20)
+        s.close()
+        out.append((img, st["raysClosest"], st["raysShadow"]))
+    for a, b in zip(out[0][0], out[1][0]):
+        assert np.array_equal(a, b)
+    assert out[0][1:] == out[1][1:]
+
+
 def test_lanes_invariance(monkeypatch):
     """Batches spread over one or two lanes (streams) give bit-identical frames."""
     imgs = []

@@ -66,6 +66,7 @@ struct GpuCtx {
       hipEvent_t done = nullptr;
       int64_t tiles = 0;
       std::vector<int64_t> frameTiles;
+      bool fused = false;  // depth 0 ran as k_trace's camera-ray instantiation
     };
     static constexpr int kPendDepth = 2;
     Pend pend[kPendDepth];
@@ -648,7 +649,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
     const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
-    const size_t counterWords = qcounter_words(levels);
+    // the queue counters, then one word: the camera rays a fused depth 0 traced (PrimaryRays)
+    const size_t counterWords = qcounter_words(levels) + 1;
+    const size_t tracedWord = counterWords - 1;
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
@@ -764,8 +767,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
             rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
           }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
-          g.stats.raysClosest += nc;
-          if (nc) g.stats.launchesClosest += 1;
+          // a fused depth 0 queues its hits only: the camera rays it traced are counted apart
+          const double traced = d == 0 && Pd.fused ? (double)Pd.hc[tracedWord] : nc;
+          g.stats.raysClosest += traced;
+          if (traced) g.stats.launchesClosest += 1;
         }
         g.stats.raysShadow += ns;
         if (d < rp.maxDepth && ns) g.stats.launchesShadow += 1;
@@ -780,6 +785,20 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     struct EvPair { hipEvent_t a, b; int kind; };
     std::vector<EvPair> evs;
     int64_t batch = 0;
+    // Depth 0 as one kernel (launch_trace_primary): camera rays generated inside the closest-hit
+    // trace, misses resolved there, only hits queued for k_shade — for static scenes whose
+    // depth-0 miss radiance is a constant: no backplate, every environment light ambient
+    // (k_shade's miss branch then adds thr * L = L per light in envLights order, thr = 1).
+    // Not in the capture frame (it copies the depth-0 queue). YRT_PRIMARY=0: k_raygen instead.
+    const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 &&
+                              !(getenv("YRT_PRIMARY") && atoi(getenv("YRT_PRIMARY")) == 0);
+    float4 missL = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j : G.hEnvLights) {
+      const float* Le = G.hLights[j].L;
+      missL.x = missL.x + 1.0f * Le[0];
+      missL.y = missL.y + 1.0f * Le[1];
+      missL.z = missL.z + 1.0f * Le[2];
+    }
     // batch boundaries (first tile of each batch, then shardTiles). YRT_TAPER=1: the last round of
     // batches (one per lane) is cut into twice as many half batches, so the lanes' final depth
     // tails are shorter and end closer together
@@ -826,13 +845,29 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         estShadow[d] = known ? (long long)es : -1;
       }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
-      launch_raygen(fv, pb, bi, st);
+      if (!fusedPrimary) launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
         EvPair e1{};
         if (kernelTiming) { e1 = {g.ev(), g.ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
-        launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                             pb.segCap, pb.hit, st, hint(estClosest[d]), pb.qTime[cur]);
+        if (d == 0 && fusedPrimary) {
+          PrimaryRays pr;
+          pr.fv = fv;
+          pr.bi = bi;
+          pr.qPath = pb.qPath[0];
+          pr.qOrg = pb.qOrg[0];
+          pr.qDir = pb.qDir[0];
+          pr.pathL = pb.pathL;
+          pr.counts = pb.counters + qcounter_index(0, 0, 0);
+          pr.segCap = pb.segCap;
+          pr.missL = missL;
+          pr.traced = pb.counters + tracedWord;
+          pr.numPaths = (long long)bi.numPixels * spp;
+          launch_trace_primary(lsv, pr, pb.hit, st);
+        } else {
+          launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
+                               pb.segCap, pb.hit, st, hint(estClosest[d]), pb.qTime[cur]);
+        }
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
           g.capture(captureMax, g.capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0),
@@ -860,6 +895,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipMemcpyAsync(Pd.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       HIP_CHECK(hipEventRecord(Pd.done, st));
       Pd.tiles = bi.numPixels / 256;
+      Pd.fused = fusedPrimary;
       Pd.frameTiles.assign(curTiles.begin(), curTiles.end());
       L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,

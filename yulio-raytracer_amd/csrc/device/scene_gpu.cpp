@@ -410,6 +410,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   }
   S->lights.upload(lights);
   S->hLights = lights;
+  S->hEnvLights = envLights;
   S->envLights.upload(envLights);
   S->media.upload(media);
 
@@ -506,6 +507,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
   R->materialMask = src.materialMask;
   R->precomputed = src.precomputed;
   R->hLights = src.hLights;
+  R->hEnvLights = src.hEnvLights;
   R->numTris = src.numTris;
   R->numGeoms = src.numGeoms;
   R->bvhDepth = src.bvhDepth;

@@ -75,6 +75,7 @@ struct GpuScene {
   std::vector<int> hTriGeom;
   std::vector<std::shared_ptr<const LightInst>> allLights;
   std::vector<GpuLight> hLights;                // the uploaded light table
+  std::vector<int> hEnvLights;                  // the uploaded envLights (indices into hLights)
   std::vector<LightSampleSource> precomputed;   // LightSampleSource per precompute() light
   // incremental commits (faceCamera refit, refit_gpu_scene): the slots this scene was built
   // from, slot -> geometry, gid -> leaf position, and the node indices grouped by tree depth

@@ -464,19 +464,29 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 // for camera rays and inherited by shadow and continuation rays, pathtraceintegrator.cpp:158,210)
 // WIDE (any-hit only): node steps on the 8-wide BVH (sv.nodes8, GpuNode8): the farthest hit
 // child next, the other hit ones pushed — fewer, wider steps per query
-template <bool ANY, bool MOTION, bool WIDE = false>
+// PRIM (closest hit, static scenes): depth 0 from the batch's path ids instead of a queue —
+// camera rays generated at refill, hits appended to the depth-0 queue, misses resolved
+// (PrimaryRays)
+template <bool ANY, bool MOTION, bool WIDE = false, bool PRIM = false>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
                                                          int segCap, float4* __restrict__ hitOut,
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
-                                                         ShadowFuse sf, const float* __restrict__ rayTime) {
+                                                         ShadowFuse sf, const float* __restrict__ rayTime,
+                                                         PrimaryRays pr) {
+  static_assert(!PRIM || (!ANY && !MOTION && !WIDE), "camera rays: closest hit, static scenes");
   constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
   __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
-  qmap_load(qm, counts, numSegs);
-  const unsigned n = qm.pre[YRT_QSEGS];
+  unsigned n;
+  if constexpr (PRIM) {
+    n = (unsigned)pr.bi.numPixels * (unsigned)const_ref(pr.fv.rp).spp;
+  } else {
+    qmap_load(qm, counts, numSegs);
+    n = qm.pre[YRT_QSEGS];
+  }
   const int lane = lane_id();
   const unsigned wavesPerBlock = YRT_TRACE_BLOCK / 64;
   const unsigned gw = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
@@ -538,12 +548,41 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // refill (or at the wave's end), instead of at every accepted hit; q = -1: nothing to store
   float bestDen = 1.f;
   q = -1;
+  const unsigned long long ltMask = (1ull << lane) - 1ull;
+  // PRIM: a finished camera ray (q = its path id) — a hit is appended with its records to the
+  // depth-0 queue segment of its path id's 64-group (one atomic per segment among the storing
+  // lanes), a miss gets the environment's radiance
+  unsigned primTraced = 0;  // camera rays this lane traced
+  auto prim_store = [&]() {
+    const bool hitp = best.tri >= 0;
+    if (!hitp) pr.pathL[q] = pr.missL;
+    const int seg = qseg_of((unsigned)q);
+    unsigned long long m = ballot(hitp);
+    while (m) {
+      const int l0 = __ffsll((long long)m) - 1;
+      const int seg0 = __builtin_amdgcn_readlane(seg, l0);
+      const unsigned long long sub = ballot(hitp && seg == seg0);
+      unsigned base = 0;
+      if (lane == l0) base = atomicAdd(pr.counts + (size_t)seg0 * YRT_QCSTRIDE, (unsigned)__popcll(sub));
+      base = (unsigned)__builtin_amdgcn_readlane((int)base, l0);
+      if (hitp && seg == seg0) {
+        const unsigned slot = (unsigned)seg0 * (unsigned)pr.segCap + base + (unsigned)__popcll(sub & ltMask);
+        pr.qPath[slot] = q;
+        pr.qOrg[slot] = ro;
+        pr.qDir[slot] = rd;
+        hitOut[slot] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
+      }
+      m &= ~sub;
+    }
+  };
 #define YRT_STORE_HIT()                                                                              \
   do {                                                                                               \
-    hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));   \
+    if constexpr (PRIM)                                                                              \
+      prim_store();                                                                                  \
+    else                                                                                             \
+      hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri)); \
     q = -1;                                                                                          \
   } while (0)
-  const unsigned long long ltMask = (1ull << lane) - 1ull;
 
 #ifdef YRT_PROFILE
   unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -564,6 +603,32 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         if (!has) {
           if (!ANY && q >= 0) YRT_STORE_HIT();
           if (li < end) {
+            if constexpr (PRIM) {
+              // k_raygen's camera ray of path li (same operations, bit-identical rays)
+              const YRT_CONST GpuRenderParams& rp = const_ref(pr.fv.rp);
+              const int p = (int)li;
+              const int smp = fastdiv(p, pr.bi.divPixels);
+              int x = 0, y = 0, f = 0;
+              const bool valid = batch_pixel(rp, pr.bi, p - smp * pr.bi.numPixels, x, y, f) && rp.maxDepth > 0 &&
+                                 !(1.0f < rp.minContribution);
+              if (valid) {
+                const GpuCamera& cam = pr.fv.cam[f];  // per lane: a wave's paths may span frames
+                const int rec = pr.fv.pixelSets[(size_t)y * rp.width + x] * rp.spp + smp;
+                const float fx = (float(x) + samp(pr.fv, 0, rec)) * rp.rcpWidth;
+                const float fy = (float(y) + samp(pr.fv, 1, rec)) * rp.rcpHeight;
+                V3 o3, d3;
+                camera_ray(cam, fx, fy, o3, d3, samp(pr.fv, 2, rec), samp(pr.fv, 3, rec));
+                ro = make_float4(o3.x, o3.y, o3.z, 0.f);
+                rd = make_float4(d3.x, d3.y, d3.z, __int_as_float(0x7f800000));
+                q = p;
+                primTraced += 1;
+              } else {
+                pr.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);  // not a pixel of the image
+                q = -1;
+                ro = make_float4(0.f, 0.f, 0.f, 1.f);  // tfar < tnear: nothing to traverse
+                rd = make_float4(0.f, 0.f, 1.f, 0.f);
+              }
+            } else {
             q = qmap_phys(qm, segCap, li);
 #if YRT_SHADOW_ORG_IDX
             if (ANY && sf.orgIdx) {
@@ -578,6 +643,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
 #endif
             rd = dir[q];
             if (MOTION) rtime = rayTime[q];
+            }
             ri = make_float4(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z), 0.f);
             ri.w = __int_as_float(plane_offsets(ri.x, ri.y, ri.z));
             {
@@ -604,6 +670,11 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         next += (unsigned)nIdle;
       } else if (nIdle == 64) {
         if (!ANY && q >= 0) YRT_STORE_HIT();
+        if constexpr (PRIM) {
+          unsigned t = primTraced;
+          for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+          if (lane == 0 && t) atomicAdd(pr.traced, t);
+        }
 #ifdef YRT_PROFILE
         if (lane == 0)
           for (int k = 0; k < 8; ++k) atomicAdd(&g_traceProfile[k], prof[k]);
@@ -1809,10 +1880,17 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
   const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   if (time)
     hipLaunchKernelGGL((k_trace<false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
-                       hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, time);
+                       hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, time, PrimaryRays{});
   else
     hipLaunchKernelGGL((k_trace<false, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                       segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr);
+                       segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr, PrimaryRays{});
+}
+
+void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
+  const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+  hipLaunchKernelGGL((k_trace<false, false, false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
+                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
+                     ShadowFuse{}, (const float*)nullptr, pr);
 }
 
 bool shadow_origin_index_built() { return YRT_SHADOW_ORG_IDX != 0; }
@@ -1827,17 +1905,17 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
   if (time) {
     if (sv.nodes8)
       hipLaunchKernelGGL((k_trace<true, true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
-                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time);
+                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});
     else
       hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time);
+                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});
   } else {
     if (sv.nodes8)
       hipLaunchKernelGGL((k_trace<true, false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
-                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr);
+                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr, PrimaryRays{});
     else
       hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr);
+                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr, PrimaryRays{});
   }
 }
 

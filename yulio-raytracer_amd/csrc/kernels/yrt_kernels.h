@@ -135,6 +135,26 @@ struct BatchInfo {
   FastDiv divPixels;   // fastdiv_make(numPixels): path id -> (sample, batch pixel)
 };
 
+// Camera rays generated inside the closest-hit kernel (k_trace<false, false, false, true>):
+// depth 0 without a raygen pass. A lane takes the batch's next path id, computes its camera ray
+// as k_raygen does, traces it and, when it is done, either appends it with its hit to the
+// depth-0 queue (qPath/qOrg/qDir/hit, the segment of its path id's 64-group) or, on a miss,
+// writes the path's radiance: the environment's (missL; direction-independent environment
+// lights only, k_shade's depth-0 miss branch). Paths outside the image get radiance 0.
+struct PrimaryRays {
+  FrameView fv;
+  BatchInfo bi;
+  int* qPath;
+  float4* qOrg;
+  float4* qDir;
+  float4* pathL;
+  unsigned* counts;   // depth-0 closest-queue counters: qcounter_index(0, 0, 0), segments YRT_QCSTRIDE apart
+  int segCap;
+  float4 missL;       // radiance of a depth-0 miss
+  unsigned* traced;   // camera rays traced (valid paths), one atomic per wave
+  long long numPaths; // numPixels * spp (grid size)
+};
+
 // Kernel launchers (kernels/pathtrace.hip)
 void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int height, int sets, hipStream_t s);
 void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s);
@@ -146,6 +166,10 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
                           int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1,
                           const float* time = nullptr);
+// depth 0 of a batch: camera rays generated, traced and queued (hits) or resolved (misses) in
+// one kernel, see PrimaryRays; replaces launch_raygen + the depth-0 launch_trace_closest for
+// static scenes without a backplate or direction-dependent environment lights
+void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s);
 // whether the kernels were built with the shared shadow-ray origins (-DYRT_SHADOW_ORG_IDX=1)
 bool shadow_origin_index_built();
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
