@@ -792,6 +792,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // Not in the capture frame (it copies the depth-0 queue). YRT_PRIMARY=0: k_raygen instead.
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 &&
                               !(getenv("YRT_PRIMARY") && atoi(getenv("YRT_PRIMARY")) == 0);
+    bool allPinhole = true;
+    for (int k = 0; k < nf; ++k) allPinhole &= g.hCams[k].type == CAM_PINHOLE;
     float4 missL = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j : G.hEnvLights) {
       const float* Le = G.hLights[j].L;
@@ -863,6 +865,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           pr.missL = missL;
           pr.traced = pb.counters + tracedWord;
           pr.numPaths = (long long)bi.numPixels * spp;
+          pr.pinholeOnly = allPinhole ? 1 : 0;
           launch_trace_primary(lsv, pr, pb.hit, st);
         } else {
           launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,

@@ -166,13 +166,17 @@ __device__ __forceinline__ A3 ldA3(const F* m) {
 // PinHoleCamera::ray (cameras/pinholecamera.h:23-25)
 // StereoCubeCamera::ray (cameras/StereoCubeCamera.h:68-161)
 // DepthOfFieldCamera::ray (cameras/depthoffieldcamera.h:20-26); (lx, ly) = the lens sample
+template <class CAM>
+__device__ __forceinline__ void pinhole_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir) {
+  A3 p2w = ldA3(cam.p2w[0]);
+  org = p2w.p;
+  dir = normalize(fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
+}
 template <class CAM>  // GpuCamera, or a YRT_CONST one (scalar loads)
 __device__ void camera_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir, float lx = 0.f,
                            float ly = 0.f) {
   if (cam.type == CAM_PINHOLE) {
-    A3 p2w = ldA3(cam.p2w[0]);
-    org = p2w.p;
-    dir = normalize(fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
+    pinhole_ray(cam, fx, fy, org, dir);
     return;
   }
   if (cam.type == CAM_DOF) {
@@ -466,8 +470,9 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 // child next, the other hit ones pushed — fewer, wider steps per query
 // PRIM (closest hit, static scenes): depth 0 from the batch's path ids instead of a queue —
 // camera rays generated at refill, hits appended to the depth-0 queue, misses resolved
-// (PrimaryRays)
-template <bool ANY, bool MOTION, bool WIDE = false, bool PRIM = false>
+// (PrimaryRays); 1: pinhole cameras only (the other cameras' code would cost registers),
+// 2: any camera
+template <bool ANY, bool MOTION, bool WIDE = false, int PRIM = 0>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
@@ -617,7 +622,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                 const float fx = (float(x) + samp(pr.fv, 0, rec)) * rp.rcpWidth;
                 const float fy = (float(y) + samp(pr.fv, 1, rec)) * rp.rcpHeight;
                 V3 o3, d3;
-                camera_ray(cam, fx, fy, o3, d3, samp(pr.fv, 2, rec), samp(pr.fv, 3, rec));
+                if constexpr (PRIM == 1)
+                  pinhole_ray(cam, fx, fy, o3, d3);
+                else
+                  camera_ray(cam, fx, fy, o3, d3, samp(pr.fv, 2, rec), samp(pr.fv, 3, rec));
                 ro = make_float4(o3.x, o3.y, o3.z, 0.f);
                 rd = make_float4(d3.x, d3.y, d3.z, __int_as_float(0x7f800000));
                 q = p;
@@ -1888,9 +1896,14 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
 
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
-  hipLaunchKernelGGL((k_trace<false, false, false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
-                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
-                     ShadowFuse{}, (const float*)nullptr, pr);
+  if (pr.pinholeOnly)
+    hipLaunchKernelGGL((k_trace<false, false, false, 1>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
+                       (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
+                       ShadowFuse{}, (const float*)nullptr, pr);
+  else
+    hipLaunchKernelGGL((k_trace<false, false, false, 2>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
+                       (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
+                       ShadowFuse{}, (const float*)nullptr, pr);
 }
 
 bool shadow_origin_index_built() { return YRT_SHADOW_ORG_IDX != 0; }

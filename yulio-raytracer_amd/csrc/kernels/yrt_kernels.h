@@ -153,6 +153,7 @@ struct PrimaryRays {
   float4 missL;       // radiance of a depth-0 miss
   unsigned* traced;   // camera rays traced (valid paths), one atomic per wave
   long long numPaths; // numPixels * spp (grid size)
+  int pinholeOnly;    // every frame's camera is a pinhole (a smaller instantiation)
 };
 
 // Kernel launchers (kernels/pathtrace.hip)
