@@ -617,15 +617,24 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
               const bool valid = batch_pixel(rp, pr.bi, p - smp * pr.bi.numPixels, x, y, f) && rp.maxDepth > 0 &&
                                  !(1.0f < rp.minContribution);
               if (valid) {
-                const GpuCamera& cam = pr.fv.cam[f];  // per lane: a wave's paths may span frames
                 const int rec = pr.fv.pixelSets[(size_t)y * rp.width + x] * rp.spp + smp;
                 const float fx = (float(x) + samp(pr.fv, 0, rec)) * rp.rcpWidth;
                 const float fy = (float(y) + samp(pr.fv, 1, rec)) * rp.rcpHeight;
-                V3 o3, d3;
-                if constexpr (PRIM == 1)
-                  pinhole_ray(cam, fx, fy, o3, d3);
-                else
-                  camera_ray(cam, fx, fy, o3, d3, samp(pr.fv, 2, rec), samp(pr.fv, 3, rec));
+                const float lx = PRIM == 1 ? 0.f : samp(pr.fv, 2, rec), ly = PRIM == 1 ? 0.f : samp(pr.fv, 3, rec);
+                V3 o3 = v3s(0.f), d3 = v3s(0.f);
+                // one pass per frame among the refilled lanes (almost always one): the frame's
+                // camera record is read with scalar loads, as in k_raygen
+                for (bool todo = true; todo;) {
+                  const int f0 = __builtin_amdgcn_readfirstlane(f);
+                  if (f == f0) {
+                    const YRT_CONST GpuCamera& cam = const_ref(pr.fv.cam + f0);
+                    if constexpr (PRIM == 1)
+                      pinhole_ray(cam, fx, fy, o3, d3);
+                    else
+                      camera_ray(cam, fx, fy, o3, d3, lx, ly);
+                    todo = false;
+                  }
+                }
                 ro = make_float4(o3.x, o3.y, o3.z, 0.f);
                 rd = make_float4(d3.x, d3.y, d3.z, __int_as_float(0x7f800000));
                 q = p;
