@@ -670,11 +670,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       }
       L.pendHead = L.pendCount = 0;
     }
-    // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH: 1 = wait for the
-    // lane's previous batch before enqueueing the next)
+    // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH, default 1: wait for
+    // the lane's previous batch — whose counters arrive before its pixel resolve — before
+    // enqueueing the next). Two ahead: C4 cube job 394 -> 429 ms on one GPU, equal at N = 8
+    // (its grid-size hints come from older batches; profiles/r04/ab_r04c.txt)
     const int pendDepth =
-        std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH"))
-                                                                                 : GpuCtx::Lane::kPendDepth));
+        std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH")) : 1));
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
     if (nl > 1) {
       hipEvent_t setup = g.ev();
