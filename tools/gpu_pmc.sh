@@ -5,6 +5,9 @@
 # usage: tools/gpu_pmc.sh <tag> ["<bench args>"]
 set -o pipefail
 export TMPDIR=/tmp
+# one frame, no warm-up: the depth-0 kernels the steady state uses on C3 (camera rays mostly hit,
+# so Device::render_shard picks k_raygen + the queued trace once it has measured that)
+export YRT_PRIMARY=${YRT_PRIMARY:-0}
 TAG=${1:-dev}
 ARGS=${2:-""}
 R=$GRAFT_REPO_ROOT

@@ -96,6 +96,9 @@ struct GpuCtx {
   // (width, height, sets) of the pixel-set map dPixelSets holds: the map depends on nothing else
   // (integratorrenderer.cpp:126-131 seeds by tile position), so a frame of the same size reuses it
   long long pixelSetsKey[3] = {-1, -1, -1};
+  // per committed scene (GpuScene::serial): the share of camera rays that left the scene in the
+  // last fused depth-0 batch (launch_trace_primary), which picks the depth-0 kernels
+  std::map<uint64_t, double> missFrac;
   std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
@@ -742,6 +745,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // device-side count, so a short estimate costs time, never correctness); YRT_HINT_PAD
     static const long long hintPad = getenv("YRT_HINT_PAD") ? atoll(getenv("YRT_HINT_PAD")) : 65536;
     auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + hintPad; };
+    auto mit = g.missFrac.find(G.serial);
+    double missEst = mit == g.missFrac.end() ? -1.0 : mit->second;
     // accounts the queue counters of the lane's oldest pending batch; without `wait` only if
     // the batch's counters have arrived (returns whether it accounted one)
     int64_t tilesDone = 0;
@@ -767,6 +772,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
             rateC[(size_t)f * levels + d] = nc / (double)Pd.tiles;
             rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
           }
+        if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
+          missEst = 1.0 - nc / (double)Pd.hc[tracedWord];
+          if (g.missFrac.size() > 64) g.missFrac.clear();
+          g.missFrac[G.serial] = missEst;
+        }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           // a fused depth 0 queues its hits only: the camera rays it traced are counted apart
           const double traced = d == 0 && Pd.fused ? (double)Pd.hc[tracedWord] : nc;
@@ -790,9 +800,14 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // trace, misses resolved there, only hits queued for k_shade — for static scenes whose
     // depth-0 miss radiance is a constant: no backplate, every environment light ambient
     // (k_shade's miss branch then adds thr * L = L per light in envLights order, thr = 1).
-    // Not in the capture frame (it copies the depth-0 queue). YRT_PRIMARY=0: k_raygen instead.
-    const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 &&
-                              !(getenv("YRT_PRIMARY") && atoi(getenv("YRT_PRIMARY")) == 0);
+    // Not in the capture frame (it copies the depth-0 queue). It pays where camera rays miss
+    // (C4: cube job -11 %) and costs where they hit (C3 -2.5 %, C5 -1.3 %: the kernel runs at 4
+    // waves/SIMD and its hits are appended scattered, profiles/r04/ab_r04d.txt), so a batch is
+    // fused while the scene's measured miss share (missFrac, from the last fused batch) is at
+    // least YRT_PRIMARY_MISS (default 0.5) or unknown. YRT_PRIMARY=0: never, 2: always.
+    const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
+    const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
+    const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
     bool allPinhole = true;
     for (int k = 0; k < nf; ++k) allPinhole &= g.hCams[k].type == CAM_PINHOLE;
     float4 missL = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -848,12 +863,13 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         estShadow[d] = known ? (long long)es : -1;
       }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
-      if (!fusedPrimary) launch_raygen(fv, pb, bi, st);
+      const bool fusedBatch = fusedPrimary && (primMode == 2 || missEst < 0 || missEst >= primMiss);
+      if (!fusedBatch) launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
         EvPair e1{};
         if (kernelTiming) { e1 = {g.ev(), g.ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
-        if (d == 0 && fusedPrimary) {
+        if (d == 0 && fusedBatch) {
           PrimaryRays pr;
           pr.fv = fv;
           pr.bi = bi;
@@ -899,7 +915,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipMemcpyAsync(Pd.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
       HIP_CHECK(hipEventRecord(Pd.done, st));
       Pd.tiles = bi.numPixels / 256;
-      Pd.fused = fusedPrimary;
+      Pd.fused = fusedBatch;
       Pd.frameTiles.assign(curTiles.begin(), curTiles.end());
       L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,
