@@ -1349,6 +1349,9 @@ __device__ __forceinline__ V3 light_sample(const LT& lt, const DG& dg, float sx,
 #ifndef YRT_SHADE_WAVES_ALL
 #define YRT_SHADE_WAVES_ALL 2  // the generic all-types instantiation (rare scenes): no spills at 2
 #endif
+#ifndef YRT_SHADE_WAVES_MP
+#define YRT_SHADE_WAVES_MP YRT_SHADE_WAVES  // instantiations with MetallicPaint (C4's set)
+#endif
 #ifdef YRT_PATH_DEBUG
 // Debug builds only (-DYRT_PATH_DEBUG): per-vertex record of one path (pixel id, sample) of the
 // shade kernel, 32 floats per depth, laid out as oracle_debug_path's (tools/c5_path_debug.py).
@@ -1367,7 +1370,9 @@ extern "C" int yrt_debug_path(int pixelId, int sample, float* out) {
 
 template <unsigned MM>
 __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
-    MM == (YRT_ALL_MATS | YRT_ALL_LIGHTS) ? YRT_SHADE_WAVES_ALL : YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
+    MM == (YRT_ALL_MATS | YRT_ALL_LIGHTS) ? YRT_SHADE_WAVES_ALL
+    : (MM & mat_bit(MAT_METALLIC_PAINT)) ? YRT_SHADE_WAVES_MP
+                                         : YRT_SHADE_WAVES))) void k_shade(SceneView sv, FrameView fv, PathBuffers pb, BatchInfo bi,
                                                    int depthLevel) {
 #ifdef YRT_SHADE_PROF
   // shader-clock cycles per phase (wave-uniform points only), summed over the waves
