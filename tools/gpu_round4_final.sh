@@ -6,6 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 T=${1:-r4f}
+bash tools/gpu_ab_cfg.sh ${T}ab "auto|-|" "never|-|YRT_PRIMARY=0" "r3|r3|" || exit $?
 timeout -k 10 480 python -u -m pytest tests -m gpu -q --maxfail=12 --timeout 200 --timeout-method thread > gpurun_out/pytest_$T.log 2>&1; rc=$?; grep -E "^FAILED|passed|failed" gpurun_out/pytest_$T.log | tail -n 14
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 bash tools/gpu_pmc.sh $T || exit $?

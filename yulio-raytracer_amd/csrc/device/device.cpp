@@ -96,9 +96,10 @@ struct GpuCtx {
   // (width, height, sets) of the pixel-set map dPixelSets holds: the map depends on nothing else
   // (integratorrenderer.cpp:126-131 seeds by tile position), so a frame of the same size reuses it
   long long pixelSetsKey[3] = {-1, -1, -1};
-  // per committed scene (GpuScene::serial): the share of camera rays that left the scene in the
-  // last fused depth-0 batch (launch_trace_primary), which picks the depth-0 kernels
-  std::map<uint64_t, double> missFrac;
+  // per committed scene (GpuScene::serial): camera rays traced by fused depth-0 batches
+  // (launch_trace_primary) and how many of them left the scene; their ratio picks the depth-0
+  // kernels (a running total: one batch's share varies with the faces it covers)
+  std::map<uint64_t, std::pair<double, double>> missFrac;
   std::map<int, DevBuf> recvSlabs;  // gather on the first device: one slab per peer
   // sample tables by request (a progressive or multi-GPU weak-scaling run cycles through a
   // few sampler iterations; rebuilding a table costs ~9 ms of host time per frame)
@@ -746,7 +747,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     static const long long hintPad = getenv("YRT_HINT_PAD") ? atoll(getenv("YRT_HINT_PAD")) : 65536;
     auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + hintPad; };
     auto mit = g.missFrac.find(G.serial);
-    double missEst = mit == g.missFrac.end() ? -1.0 : mit->second;
+    double missEst = mit == g.missFrac.end() ? -1.0 : mit->second.first / mit->second.second;
     // accounts the queue counters of the lane's oldest pending batch; without `wait` only if
     // the batch's counters have arrived (returns whether it accounted one)
     int64_t tilesDone = 0;
@@ -773,9 +774,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
             rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
           }
         if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
-          missEst = 1.0 - nc / (double)Pd.hc[tracedWord];
-          if (g.missFrac.size() > 64) g.missFrac.clear();
-          g.missFrac[G.serial] = missEst;
+          if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
+          auto& acc = g.missFrac[G.serial];
+          acc.first += (double)Pd.hc[tracedWord] - nc;
+          acc.second += (double)Pd.hc[tracedWord];
+          missEst = acc.first / acc.second;
         }
         if (d < rp.maxDepth) {  // level maxDepth counts continuations that are never traced
           // a fused depth 0 queues its hits only: the camera rays it traced are counted apart
@@ -803,7 +806,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // Not in the capture frame (it copies the depth-0 queue). It pays where camera rays miss
     // (C4: cube job -11 %) and costs where they hit (C3 -2.5 %, C5 -1.3 %: the kernel runs at 4
     // waves/SIMD and its hits are appended scattered, profiles/r04/ab_r04d.txt), so a batch is
-    // fused while the scene's measured miss share (missFrac, from the last fused batch) is at
+    // fused while the scene's measured miss share (missFrac, over its fused batches so far) is at
     // least YRT_PRIMARY_MISS (default 0.5) or unknown. YRT_PRIMARY=0: never, 2: always.
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
