@@ -1,7 +1,6 @@
-# round-4 end-state evidence: GPU suite, PMC passes of the C3 bench workload
-# (-> profiles/pmc_c3.json), the default bench line reading them, its rocprof split, the C4
-# cube-job rank shares for N = 1, 2, 4, 8 with the C4 and C3 kernel splits, the N=2 gloo
-# rehearsal line, every BASELINE config, and C5 render-only
+# round-4 end-state evidence, part 1: a same-box A/B of the depth-0 choice and the round-3 build,
+# the GPU suite, PMC passes of the C3 bench workload (-> profiles/pmc_c3.json), the default bench
+# line reading them and its rocprof split (part 2: tools/gpu_round4_final2.sh)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -16,15 +15,3 @@ cut -c1-240 gpurun_out/bench_$T.json
 cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- \
   python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench_prof_$T.json 2> $R/gpurun_out/bench_prof_$T.err || exit $?
 cd $R && python3 tools/kstats_csv.py gpurun_out/prof_$T 6
-timeout -k 10 300 python -u tools/cube_shard_time.py C4 --mode cube --gpus 1,2,4,8 > gpurun_out/c4_$T.log 2>&1 || exit $?
-grep '^{' gpurun_out/c4_$T.log | cut -c1-200
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4_$T -o run -- \
-  python3 $R/tools/cube_shard_time.py C4 --mode cube --gpus 1 > $R/gpurun_out/prof_c4_$T.log 2>&1 || exit $?
-cd $R && python3 tools/kstats_csv.py gpurun_out/prof_c4_$T 6
-YRT_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29543 bench.py --gpus 2 --steps 2 --warmup 1 > gpurun_out/bench_n2_$T.json 2> gpurun_out/bench_n2_$T.err || exit $?
-grep "^{" gpurun_out/bench_n2_$T.json | cut -c1-200
-timeout -k 10 400 python -u tools/configs_bench.py > gpurun_out/configs_$T.txt 2>&1 || exit $?
-tail -n 8 gpurun_out/configs_$T.txt
-timeout -k 10 400 python -u tools/c5_bench.py --no-face --no-startrt --no-cpu --out gpurun_out/c5_$T.json > gpurun_out/c5_$T.log 2>&1 || exit $?
-tail -n 2 gpurun_out/c5_$T.log | cut -c1-300
