@@ -315,11 +315,12 @@ def test_batch_capacity_invariance(gpu_device, monkeypatch):
 
 @pytest.mark.parametrize("which", ["C3", "C4"])
 def test_fused_primary_invariance(gpu_device, monkeypatch, which):
-    """Depth 0 as one kernel (camera rays generated and misses resolved inside the closest-hit
-    trace, launch_trace_primary) against k_raygen + the queued trace: bit-identical frames and
-    the same query counts; C3's dome and C4's zero HDRI both take the fused path."""
+    """Depth 0 as one kernel (camera rays generated inside the closest-hit trace,
+    launch_trace_primary) — hits compacted and misses resolved there (YRT_PRIMARY=2), or every
+    path in its own slot (identity layout, 3) — against k_raygen + the queued trace (0):
+    bit-identical frames and the same query counts; C3's dome and C4's zero HDRI both qualify."""
     out = []
-    for prim in ("0", "2"):
+    for prim in ("0", "2", "3"):
         monkeypatch.setenv("YRT_PRIMARY", prim)
         gpu_device.set_batch_capacity(256 * 16 * 5)  # several batches on both lanes
         try:
@@ -334,9 +335,10 @@ def test_fused_primary_invariance(gpu_device, monkeypatch, which):
             gpu_device.set_batch_capacity(64 << 20)
         s.close()
         out.append((img, st["raysClosest"], st["raysShadow"]))
-    for a, b in zip(out[0][0], out[1][0]):
-        assert np.array_equal(a, b)
-    assert out[0][1:] == out[1][1:]
+    for o in out[1:]:
+        for a, b in zip(out[0][0], o[0]):
+            assert np.array_equal(a, b)
+        assert out[0][1:] == o[1:]
 
 
 def test_lanes_invariance(monkeypatch):

@@ -653,9 +653,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
     const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
-    // the queue counters, then one word: the camera rays a fused depth 0 traced (PrimaryRays)
-    const size_t counterWords = qcounter_words(levels) + 1;
-    const size_t tracedWord = counterWords - 1;
+    // the queue counters, then two words: the camera rays a fused depth 0 traced and how many
+    // of them hit (PrimaryRays::traced)
+    const size_t counterWords = qcounter_words(levels) + 2;
+    const size_t tracedWord = counterWords - 2, hitsWord = counterWords - 1;
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
@@ -776,7 +777,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
           if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
           auto& acc = g.missFrac[G.serial];
-          acc.first += (double)Pd.hc[tracedWord] - nc;
+          acc.first += (double)Pd.hc[tracedWord] - (double)Pd.hc[hitsWord];
           acc.second += (double)Pd.hc[tracedWord];
           missEst = acc.first / acc.second;
         }
@@ -811,6 +812,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
+    const bool primIdentity = getenv("YRT_PRIMARY_IDENTITY") && atoi(getenv("YRT_PRIMARY_IDENTITY")) != 0;
+    const bool identityOk = rp.maxDepth > 0 && !(1.0f < rp.minContribution);
     bool allPinhole = true;
     for (int k = 0; k < nf; ++k) allPinhole &= g.hCams[k].type == CAM_PINHOLE;
     float4 missL = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -866,7 +869,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         estShadow[d] = known ? (long long)es : -1;
       }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
-      const bool fusedBatch = fusedPrimary && (primMode == 2 || missEst < 0 || missEst >= primMiss);
+      // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
+      // YRT_PRIMARY_IDENTITY=1 for the scenes whose rays mostly hit) or k_raygen otherwise
+      const bool compactBatch = primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss));
+      const bool identityBatch = !compactBatch && identityOk && (primMode == 3 || (primMode == 1 && primIdentity));
+      const bool fusedBatch = fusedPrimary && (compactBatch || identityBatch);
       if (!fusedBatch) launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
@@ -886,6 +893,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           pr.traced = pb.counters + tracedWord;
           pr.numPaths = (long long)bi.numPixels * spp;
           pr.pinholeOnly = allPinhole ? 1 : 0;
+          pr.identity = compactBatch ? 0 : 1;
           launch_trace_primary(lsv, pr, pb.hit, st);
         } else {
           launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
