@@ -5,6 +5,8 @@ export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 T=${1:-r4f}
 timeout -k 10 300 python -u tools/cube_shard_time.py C4 --mode cube --gpus 1,2,4,8 > gpurun_out/c4_$T.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/cube_shard_time.py C4 --mode cube --gpus 1,8 --capacity 134217728 > gpurun_out/c4cap_$T.log 2>&1 || exit $?
+grep "^{" gpurun_out/c4cap_$T.log | cut -c1-200
 grep '^{' gpurun_out/c4_$T.log | cut -c1-200
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4_$T -o run -- \
   python3 $R/tools/cube_shard_time.py C4 --mode cube --gpus 1 > $R/gpurun_out/prof_c4_$T.log 2>&1 || exit $?
