@@ -15,5 +15,5 @@ cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format cs
   python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/bench_prof_r4a.json 2> $R/gpurun_out/bench_prof_r4a.err || exit $?
 cd $R && python3 tools/kstats_csv.py gpurun_out/prof_r4a 5
 bash tools/gpu_env_ab.sh oi YRT_SHADOW_ORG_IDX=0 YRT_SHADOW_ORG_IDX=1 2 || exit $?
-bash tools/gpu_round4_c4.sh || exit $?
+bash tools/batches/r04/gpu_round4_c4.sh || exit $?
 bash tools/gpu_kstats.sh nu || exit $?

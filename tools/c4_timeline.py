@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Kernel timeline of the last render in a rocprofv3 kernel trace (tools/gpu_round4_c4b.sh):
+"""Kernel timeline of the last render in a rocprofv3 kernel trace (tools/batches/r04/gpu_round4_c4b.sh):
 the job's span, how much of it the GPU runs kernels on one lane, on both, or on none, the
 small (near-empty) launches and the tail after the last raygen.
 
