@@ -305,11 +305,15 @@ def test_batch_capacity_invariance(gpu_device, monkeypatch):
         monkeypatch.delenv("YRT_PEND_DEPTH")
         monkeypatch.setenv("YRT_TAPER", "1")
         d = s.render()
+        monkeypatch.delenv("YRT_TAPER")
+        monkeypatch.setenv("YRT_LANE_ORDER", "rr")  # batches dealt to the lanes in turn
+        e = s.render()
     finally:
         gpu_device.set_batch_capacity(64 << 20)
     assert np.array_equal(a, b)
     assert np.array_equal(a, c)
     assert np.array_equal(a, d)
+    assert np.array_equal(a, e)
     s.close()
 
 

@@ -679,6 +679,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // the lane's previous batch — whose counters arrive before its pixel resolve — before
     // enqueueing the next). Two ahead: C4 cube job 394 -> 429 ms on one GPU, equal at N = 8
     // (its grid-size hints come from older batches; profiles/r04/ab_r04c.txt)
+    const bool laneRoundRobin = getenv("YRT_LANE_ORDER") && strcmp(getenv("YRT_LANE_ORDER"), "rr") == 0;
     const int pendDepth =
         std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH")) : 1));
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
@@ -839,11 +840,26 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     for (size_t bix = 0; bix + 1 < bounds.size(); ++bix, ++batch) {
       const int64_t first = bounds[bix], batchTiles = bounds[bix + 1] - first;
       if (R.stopFlag && R.stopFlag->load()) break;
-      GpuCtx::Lane& L = g.lanes[batch % nl];
-      // account the batches that have finished, then make room in this lane's ring
-      for (int l = 0; l < nl; ++l)
-        while (drain_one(g.lanes[l], false)) {}
-      while (L.pendCount >= pendDepth) drain_one(L, true);
+      // the batch goes to the first lane with room in its ring (the fewest pending batches):
+      // finished batches are accounted as they arrive, on any lane, so a lane that finishes
+      // early is refilled at once instead of waiting for the other lane's older batch
+      // (round-robin lanes with one batch ahead: C4 N = 3 rank share 160 ms, YRT_LANE_ORDER=rr)
+      int li = -1;
+      for (;;) {
+        for (int l = 0; l < nl; ++l)
+          while (drain_one(g.lanes[l], false)) {}
+        if (laneRoundRobin) {
+          GpuCtx::Lane& R0 = g.lanes[batch % nl];
+          if (R0.pendCount < pendDepth) { li = (int)(batch % nl); break; }
+          drain_one(R0, true);
+          continue;
+        }
+        for (int l = 0; l < nl; ++l)
+          if (g.lanes[l].pendCount < pendDepth && (li < 0 || g.lanes[l].pendCount < g.lanes[li].pendCount)) li = l;
+        if (li >= 0) break;
+        std::this_thread::yield();
+      }
+      GpuCtx::Lane& L = g.lanes[li];
       const hipStream_t st = L.stream;
       const PathBuffers pb = lane_buffers(L);
       SceneView lsv = sv;
