@@ -727,6 +727,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // a cube job's batch after a face change would otherwise get another face's grids.
     const bool useHints = !getenv("YRT_NO_GRID_HINTS");
     std::vector<double> rateC((size_t)nf * levels, -1.0), rateS((size_t)nf * levels, -1.0);
+    // YRT_HINT_MODE=max: a batch's hint is the highest rate per tile any drained batch of the
+    // job had at that depth, times its tiles (never below a band of the frame seen before)
+    const bool hintMax = getenv("YRT_HINT_MODE") && strcmp(getenv("YRT_HINT_MODE"), "max") == 0;
+    std::vector<double> maxRateC(levels, -1.0), maxRateS(levels, -1.0);
     // the batch's tiles per frame: shard tile j of the batch is job tile index + j * count
     auto frame_tiles = [&](int64_t firstTile, int64_t ntiles, int64_t* per) {
       for (int f = 0; f < nf; ++f) per[f] = 0;
@@ -775,6 +779,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
             rateC[(size_t)f * levels + d] = nc / (double)Pd.tiles;
             rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
           }
+        maxRateC[d] = std::max(maxRateC[d], nc / (double)Pd.tiles);
+        maxRateS[d] = std::max(maxRateS[d], ns / (double)Pd.tiles);
         if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
           if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
           auto& acc = g.missFrac[G.serial];
@@ -883,6 +889,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         }
         estClosest[d] = known ? (long long)ec : -1;
         estShadow[d] = known ? (long long)es : -1;
+        if (hintMax) {
+          estClosest[d] = maxRateC[d] >= 0 ? (long long)(maxRateC[d] * (double)batchTiles) : -1;
+          estShadow[d] = maxRateS[d] >= 0 ? (long long)(maxRateS[d] * (double)batchTiles) : -1;
+        }
       }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
       // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
