@@ -721,11 +721,15 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.fuseShadow = numDirect == 1 && !getenv("YRT_NO_SHADOW_FUSE");
       return pb;
     };
-    // grid-size hints: queue entries per tile of the drained batches, per frame and depth;
-    // a batch's hint is the sum over its frames of rate x tiles (-1 = a frame without a rate
-    // yet, full grids). Per frame because queue lengths differ between faces (sky vs floor):
-    // a cube job's batch after a face change would otherwise get another face's grids.
-    const bool useHints = !getenv("YRT_NO_GRID_HINTS");
+    // grid-size hints (YRT_GRID_HINTS=1; off by default): queue entries per tile of the drained
+    // batches, per frame and depth; a batch's hint is the sum over its frames of rate x tiles
+    // (-1 = a frame without a rate yet, full grids). Off: every launch gets the full grid (its
+    // waves grid-stride over the device-side count and idle ones exit at once). Round 4 measured
+    // the hints a loss: a band of a face inherits the previous band's rates (sky above, floor
+    // below), so grids come out too small; without them C4 runs 389 -> 371 ms on one GPU and
+    // its N = 2 / 3 rank shares 215 -> 189 / 162 -> 128 ms, C3 and N = 8 unchanged, and larger
+    // pads converge to the same (profiles/r04/ab_r04j.txt)
+    const bool useHints = getenv("YRT_GRID_HINTS") && atoi(getenv("YRT_GRID_HINTS")) != 0;
     std::vector<double> rateC((size_t)nf * levels, -1.0), rateS((size_t)nf * levels, -1.0);
     // YRT_HINT_MODE=max: a batch's hint is the highest rate per tile any drained batch of the
     // job had at that depth, times its tiles (never below a band of the frame seen before)
