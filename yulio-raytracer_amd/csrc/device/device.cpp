@@ -677,8 +677,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     }
     // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH, default 1: wait for
     // the lane's previous batch — whose counters arrive before its pixel resolve — before
-    // enqueueing the next). Two ahead: C4 cube job 394 -> 429 ms on one GPU, equal at N = 8
-    // (its grid-size hints come from older batches; profiles/r04/ab_r04c.txt)
+    // enqueueing the next). Two ahead measured equal with full grids (profiles/r04/ab_r04k.txt)
     const bool laneRoundRobin = getenv("YRT_LANE_ORDER") && strcmp(getenv("YRT_LANE_ORDER"), "rr") == 0;
     const int pendDepth =
         std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH")) : 1));
