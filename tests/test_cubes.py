@@ -90,6 +90,25 @@ def test_cube_job_shards_compose(gpu_device):
 
 
 @pytest.mark.gpu
+def test_batch_grow_invariance(gpu_device, monkeypatch):
+    """A rank's share of the full-size C4 cube job at N = 8 runs 7 batches per lane at the default
+    capacity, so Device::render_shard grows it to 4 larger ones; the faces are bit-identical to
+    the share rendered without growing (YRT_BATCH_GROW=0)."""
+    s = yrt.Session(c4_args() + ["-fb", "RGB8"], device=gpu_device)
+    faces = []
+    try:
+        gpu_device.set_tile_shard(3, 8)
+        for grow in ("0", "1"):
+            monkeypatch.setenv("YRT_BATCH_GROW", grow)
+            faces.append(s.render_cube())
+    finally:
+        gpu_device.set_tile_shard(0, 1)
+    s.close()
+    for a, b in zip(faces[0], faces[1]):
+        assert a.any() and np.array_equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fb", ["RGB_FLOAT32", "RGB8"])
 def test_cube_job_multi_device(gpu_device, fb):
     """devices=0,0,0 (three logical shards, slab gather on the first; RGB8 framebuffers move

@@ -646,6 +646,16 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     if (captureMax == 0 && g.numLanes > 1 && shardTiles > 1) {
       int64_t nb = (shardTiles + tilesPerBatch - 1) / tilesPerBatch;
       nb = (nb + g.numLanes - 1) / g.numLanes * g.numLanes;
+      // At the default capacity, a lane that would run 5-8 batches runs half as many of twice
+      // the size: each batch pays a fixed chain of 10 depths x 3 launches and a ramp-down, which
+      // outweighs the overlap the extra batches buy there (C4 N = 8 rank share 51.0 -> 48.7 ms;
+      // at 27+ batches per lane, N = 1 / 2, twice the size measured +1 / +4 %,
+      // profiles/r04/ab_r04k.txt, scaling_prediction_c4_r04z.txt). YRT_BATCH_GROW=0: off.
+      const bool grow = capacity == ((int64_t)YRT_DEFAULT_CAPACITY_M << 20) &&
+                        !(getenv("YRT_BATCH_GROW") && atoi(getenv("YRT_BATCH_GROW")) == 0);
+      if (grow && nb > 4 * g.numLanes && nb <= 8 * g.numLanes) {
+        nb = (nb / 2 + g.numLanes - 1) / g.numLanes * g.numLanes;
+      }
       tilesPerBatch = (shardTiles + nb - 1) / nb;
     }
     const int64_t P = std::min<int64_t>(tilesPerBatch, shardTiles) * 256 * spp;
