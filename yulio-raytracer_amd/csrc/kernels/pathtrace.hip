@@ -426,6 +426,9 @@ __device__ unsigned long long g_traceProfile[8];
 // +0.6 % on C3 over code scheduled for 5 (profiles/r01/variants_r01.txt)
 #define YRT_TRACE_WAVES 6
 #endif
+#ifndef YRT_TRACE_WAVES_PRIM
+#define YRT_TRACE_WAVES_PRIM YRT_TRACE_WAVES  // the camera-ray (fused depth-0) instantiations
+#endif
 #ifndef YRT_TRACE_WAVES_ANY
 #define YRT_TRACE_WAVES_ANY YRT_TRACE_WAVES  // occupancy target of the shadow-ray instantiation
 #endif
@@ -473,7 +476,8 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 // (PrimaryRays); 1 / 3: pinhole cameras only (the other cameras' code would cost registers),
 // 2 / 4: any camera; 3 / 4: identity layout (PrimaryRays::identity), 1 / 2: hits compacted
 template <bool ANY, bool MOTION, bool WIDE = false, int PRIM = 0>
-__global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(ANY ? YRT_TRACE_WAVES_ANY : YRT_TRACE_WAVES))) void k_trace(
+__global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(
+    ANY ? YRT_TRACE_WAVES_ANY : PRIM ? YRT_TRACE_WAVES_PRIM : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
                                                          const float4* __restrict__ dir,
                                                          const unsigned* __restrict__ counts, int numSegs,
