@@ -20,6 +20,7 @@ Per kernel, averaged over its dispatches:
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -37,7 +38,11 @@ def per_dispatch(dirs):
         for f in Path(d).rglob("*counter_collection.csv"):
             for row in csv.DictReader(open(f)):
                 name = row.get("Kernel_Name", "")
+                # the fused depth-0 instantiations (k_trace<false, false, false, 1..4>) apart
+                prim = re.search(r"k_trace<false, \w+, \w+, [1-4]>", name) is not None
                 for k, tag in KERNELS.items():
+                    if k == "k_trace<false>" and prim:
+                        k = "k_trace<false> depth 0 fused"
                     if tag in name:
                         c = row["Counter_Name"]
                         acc[k][c] += float(row["Counter_Value"] or 0)
