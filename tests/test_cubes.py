@@ -90,14 +90,15 @@ def test_cube_job_shards_compose(gpu_device):
 
 
 @pytest.mark.gpu
-def test_batch_grow_invariance(gpu_device, monkeypatch):
-    """A rank's share of the full-size C4 cube job at N = 8 runs 7 batches per lane at the default
-    capacity, so Device::render_shard grows it to 4 larger ones; the faces are bit-identical to
-    the share rendered without growing (YRT_BATCH_GROW=0)."""
+@pytest.mark.parametrize("n", [8, 4])
+def test_batch_grow_invariance(gpu_device, monkeypatch, n):
+    """A rank's share of the full-size C4 cube job runs 7 (N = 8) or 14 (N = 4) batches per lane
+    at the default capacity, so Device::render_shard grows them to 2x / 1.5x the size; the faces
+    are bit-identical to the share rendered without growing (YRT_BATCH_GROW=0)."""
     s = yrt.Session(c4_args() + ["-fb", "RGB8"], device=gpu_device)
     faces = []
     try:
-        gpu_device.set_tile_shard(3, 8)
+        gpu_device.set_tile_shard(n - 1, n)
         for grow in ("0", "1"):
             monkeypatch.setenv("YRT_BATCH_GROW", grow)
             faces.append(s.render_cube())

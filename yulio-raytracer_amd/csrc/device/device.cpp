@@ -655,6 +655,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                         !(getenv("YRT_BATCH_GROW") && atoi(getenv("YRT_BATCH_GROW")) == 0);
       if (grow && nb > 4 * g.numLanes && nb <= 8 * g.numLanes) {
         nb = (nb / 2 + g.numLanes - 1) / g.numLanes * g.numLanes;
+      } else if (grow && nb > 8 * g.numLanes && nb <= 16 * g.numLanes) {
+        // 9-16 per lane: 1.5x the size (C4 N = 4 share, 96 M paths: 100 -> 95 ms, ab_r04k.txt)
+        nb = (nb * 2 / 3 + g.numLanes - 1) / g.numLanes * g.numLanes;
       }
       tilesPerBatch = (shardTiles + nb - 1) / nb;
     }
