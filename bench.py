@@ -63,9 +63,31 @@ def parse():
     return p.parse_args()
 
 
+def launch_ranks(a):
+    """`bench.py --gpus N` (N > 1) started without a launcher: this process has not touched the
+    GPU (no torch import yet), so it starts the N ranks itself as the driver would —
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same arguments>` on 127.0.0.1 —
+    lets rank 0's JSON line through on the shared stdout and exits with the launcher's status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ, YRT_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child ranks)")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit(f"--gpus {a.gpus}: at least one GPU")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit(f"WORLD_SIZE={world} but --gpus {a.gpus}: the launcher's rank count and --gpus must agree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -240,6 +262,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "gather": gather,
+            "launcher": os.environ.get("YRT_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none"),
             "stereo_cubemap": stereo,
         }
         print(json.dumps(out), flush=True)

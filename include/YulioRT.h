@@ -17,11 +17,87 @@
 #ifndef YULIO_RT_H
 #define YULIO_RT_H
 
-#ifdef __cplusplus
-extern "C" {
-#endif
-
 #define YULIO_DLL_EXPORT __attribute__((visibility("default")))
+
+#ifdef __cplusplus
+/* C++: the declarations live in namespace Yulio as in the reference header (YulioRT.h:9-58),
+ * so a caller written against it (rt_test_dll/rt_test_dll.cpp:10 `using namespace Yulio;`, or
+ * `Yulio::StartRT(...)`) compiles unchanged. The functions keep C linkage: extern "C" inside a
+ * namespace binds the plain symbols StartRT, WaitRT, ... that C and ctypes callers use. */
+namespace Yulio {
+
+enum ErrorCodeRT {
+  NoError = 0,
+  RenderingIsInProgress,
+  MissingColladaFile,
+  InvalidColladaFormat,
+  UnitializedRenderer,
+  FailedToPopulateStatus,
+  UnknownError = 1000
+};
+
+enum StateRT { Inactive, Initialiazing, Rendering, Stopped, Done };
+
+struct StatusRT {
+  StateRT state;
+  float progress; /* [0,1] */
+  ErrorCodeRT lastError;
+};
+
+struct ParamsRT {
+  const char* renderer = "pathtracer";
+  int size = 1536;
+  int depth = 10;
+  float tMaxShadowRay = 120.f;
+  int spp = 256;
+  float ambientlight[3] = {.83f, .95f, .98f};
+  float eyeSeparation = 2.5f;
+  bool toeIn = true;
+  float zeroParallax = 75.f;
+  int jpegQuality = 90;
+  bool debug = false;
+  int threadsPriority = 0;
+  bool waterMark = false;
+  const char* faceCullingMode = "default";
+};
+
+extern "C" {
+YULIO_DLL_EXPORT bool StartRT(const char* colladaFile, const ParamsRT* params);
+YULIO_DLL_EXPORT bool WaitRT();
+YULIO_DLL_EXPORT bool StopRT(bool keepResults);
+YULIO_DLL_EXPORT ErrorCodeRT GetLastErrorRT();
+YULIO_DLL_EXPORT void GetCurrentStatusRT(StatusRT* status);
+/* Extension for C callers: fills the default member initializers above. */
+YULIO_DLL_EXPORT void InitParamsRT(ParamsRT* params);
+}
+
+}  // namespace Yulio
+
+/* Global names for callers of this build that predate the namespace (the same entities). */
+using Yulio::ErrorCodeRT;
+using Yulio::NoError;
+using Yulio::RenderingIsInProgress;
+using Yulio::MissingColladaFile;
+using Yulio::InvalidColladaFormat;
+using Yulio::UnitializedRenderer;
+using Yulio::FailedToPopulateStatus;
+using Yulio::UnknownError;
+using Yulio::StateRT;
+using Yulio::Inactive;
+using Yulio::Initialiazing;
+using Yulio::Rendering;
+using Yulio::Stopped;
+using Yulio::Done;
+using Yulio::StatusRT;
+using Yulio::ParamsRT;
+using Yulio::StartRT;
+using Yulio::WaitRT;
+using Yulio::StopRT;
+using Yulio::GetLastErrorRT;
+using Yulio::GetCurrentStatusRT;
+using Yulio::InitParamsRT;
+
+#else /* C */
 
 typedef enum ErrorCodeRT {
   NoError = 0,
@@ -41,23 +117,8 @@ typedef struct StatusRT {
   ErrorCodeRT lastError;
 } StatusRT;
 
+/* Same layout as the C++ struct; InitParamsRT fills its defaults. */
 typedef struct ParamsRT {
-#ifdef __cplusplus
-  const char* renderer = "pathtracer";
-  int size = 1536;
-  int depth = 10;
-  float tMaxShadowRay = 120.f;
-  int spp = 256;
-  float ambientlight[3] = {.83f, .95f, .98f};
-  float eyeSeparation = 2.5f;
-  bool toeIn = true;
-  float zeroParallax = 75.f;
-  int jpegQuality = 90;
-  bool debug = false;
-  int threadsPriority = 0;
-  bool waterMark = false;
-  const char* faceCullingMode = "default";
-#else
   const char* renderer;
   int size;
   int depth;
@@ -72,26 +133,15 @@ typedef struct ParamsRT {
   int threadsPriority;
   _Bool waterMark;
   const char* faceCullingMode;
-#endif
 } ParamsRT;
 
-/* C callers: fills the C++ default member initializers above. */
 YULIO_DLL_EXPORT void InitParamsRT(ParamsRT* params);
-
-#ifdef __cplusplus
-YULIO_DLL_EXPORT bool StartRT(const char* colladaFile, const ParamsRT* params);
-YULIO_DLL_EXPORT bool WaitRT();
-YULIO_DLL_EXPORT bool StopRT(bool keepResults);
-#else
 YULIO_DLL_EXPORT _Bool StartRT(const char* colladaFile, const ParamsRT* params);
 YULIO_DLL_EXPORT _Bool WaitRT(void);
 YULIO_DLL_EXPORT _Bool StopRT(_Bool keepResults);
-#endif
 YULIO_DLL_EXPORT ErrorCodeRT GetLastErrorRT(void);
 YULIO_DLL_EXPORT void GetCurrentStatusRT(StatusRT* status);
 
-#ifdef __cplusplus
-}
-#endif
+#endif /* __cplusplus */
 
 #endif /* YULIO_RT_H */

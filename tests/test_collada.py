@@ -8,6 +8,7 @@ missing blobs), so the loader is pinned against the restated Assimp/DAELoader ru
 "parity unpinned" against the reference's own importer output."""
 import numpy as np
 import pytest
+from pathlib import Path
 
 import dae_scene
 import oracle
@@ -192,6 +193,63 @@ def test_rt_test_dll_usage():
     exe = Path(__file__).resolve().parent.parent / "yulio-raytracer_amd" / "lib" / "rt_test_dll"
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_rt_test_dll_cpp_usage():
+    """The C++ DLL driver, written like the reference's caller (`using namespace Yulio;`,
+    rt_test_dll/rt_test_dll.cpp:10), links and prints its usage without a scene."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "yulio-raytracer_amd" / "lib" / "rt_test_dll_cpp"
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+REF_CALLER = Path("/root/reference/rt_test_dll/rt_test_dll.cpp")
+
+
+@pytest.mark.skipif(not REF_CALLER.exists(), reason="the reference tree is only in the build container")
+def test_reference_caller_compiles_against_header(tmp_path):
+    """The reference's own caller, unchanged, compiles and links against include/YulioRT.h and
+    libYulioRT_mi355x.so (devices/renderer/YulioRT.h:9-58: namespace Yulio, extern "C" entry
+    points). The source is piped to the compiler as text, so its quoted includes resolve
+    against -I: "stdafx.h" (the MSVC precompiled header, empty here) and
+    "../devices/renderer/YulioRT.h" -> this build's header. The program is linked, not run (it
+    renders a hard-coded absent .dae)."""
+    import subprocess
+    root = Path(__file__).resolve().parent.parent
+    inc = tmp_path / "inc"
+    (tmp_path / "devices" / "renderer").mkdir(parents=True)
+    inc.mkdir()
+    (inc / "stdafx.h").write_text("")
+    (tmp_path / "devices" / "renderer" / "YulioRT.h").symlink_to(root / "include" / "YulioRT.h")
+    lib = root / "yulio-raytracer_amd" / "lib"
+    exe = tmp_path / "rt_test_dll_ref"
+    r = subprocess.run(["g++", "-std=c++14", "-x", "c++", "-", "-I", str(inc), "-o", str(exe), "-L", str(lib),
+                        "-lYulioRT_mi355x", "-Wl,-rpath," + str(lib), "-lpthread"],
+                       input=REF_CALLER.read_text(errors="replace"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert exe.exists()
+
+
+@pytest.mark.gpu
+def test_rt_test_dll_cpp_renders(tmp_path):
+    """The C++ driver (using namespace Yulio; ParamsRT with the reference caller's overrides;
+    StartRT -> WaitRT twice, rt_test_dll.cpp:14-41) renders the Collada scene's FPR views, and
+    its watermarked strips equal the plain-C driver's byte for byte."""
+    import subprocess
+    lib = Path(__file__).resolve().parent.parent / "yulio-raytracer_amd" / "lib"
+    a, b = tmp_path / "cpp", tmp_path / "c"
+    fa, fb = dae_scene.write(a), dae_scene.write(b)
+    r = subprocess.run([str(lib / "rt_test_dll_cpp"), str(fa), "32", "2", "2"], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("state 4") == 2, r.stdout  # Done, both iterations
+    r = subprocess.run([str(lib / "rt_test_dll"), str(fb), "32", "2", "--watermark"], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for view in ("room_Kitchen.jpg", "room_Hall.jpg"):
+        assert (a / view).read_bytes() == (b / view).read_bytes()
 
 
 @pytest.mark.gpu

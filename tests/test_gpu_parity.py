@@ -292,6 +292,34 @@ def test_tile_shards_compose_bit_exact(gpu_device):
     s.close()
 
 
+def test_multi_device_tile_shards_compose_bit_exact(gpu_device):
+    """A process of two logical devices (devices=0,0) rendering a process-level shard
+    (yrtSetTileShard(k, 3), no communicator): the pixels of the other processes' shards read as
+    zeros in every render, including a fresh frame block and one that held a whole frame, so the
+    three per-process images sum to the one-device frame (device.cpp shard clear)."""
+    from yrt.dist import tile_mask
+    args = c2_args(200, 4) + ["-fb", "RGB_FLOAT32"]
+    s = yrt.Session(args, device=gpu_device)
+    full = s.render()
+    s.close()
+    multi = yrt.Device(devices=[0, 0])
+    try:
+        s = yrt.Session(args, device=multi)
+        assert np.array_equal(s.render(), full)  # the block now holds a whole frame
+        parts = []
+        for k in range(3):
+            multi.set_tile_shard(k, 3)
+            parts.append(s.render())
+            assert np.array_equal(s.render(), parts[-1])
+        multi.set_tile_shard(0, 1)
+        s.close()
+    finally:
+        multi.close()
+    for k, p in enumerate(parts):
+        assert not p[~tile_mask(200, 200, k, 3)].any(), k
+    assert np.array_equal(sum(parts), full)
+
+
 def test_batch_capacity_invariance(gpu_device, monkeypatch):
     s = _session(gpu_device, c2_args(160, 4))
     a = s.render()

@@ -405,7 +405,11 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     }
     std::vector<GpuScene*> scenes(nr);
     for (int k = 0; k < nr; ++k) scenes[k] = &scene_on(S, ctx[k]->hipDevice, k == 0);
-    shardZero = nr == 1 && !procGather;
+    // Without a process gather, the pixels of the other processes' shards (yrtSetTileShard)
+    // must read as zeros so per-process images compose by sum: ctx[0]'s block is cleared
+    // outside the tiles this call writes. With several devices in the process and no
+    // process-level shard (shardCount 1), the local gather writes every tile: no clear.
+    shardZero = !procGather && (nr == 1 || shardCount > 1);
     if (nr == 1) {
       render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
     } else {
@@ -588,9 +592,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   B.fbRGB8.alloc((size_t)nf * rgb8Stride * H);
   const long long zkey[5] = {index, count, W, H, nf};
   if (B.fbFloat.p != oldF || B.fbRGB8.p != oldB) B.zeroKey[0] = -1;
-  if (count > 1 && shardZero && !R.debug) {
+  if (count > 1 && shardZero && &g == ctx[0].get() && !R.debug) {
     // pixels of other shards stay 0 so per-shard images compose by sum; a block that already
-    // holds this layout's zeros (the same shard rendered into it before) is not cleared again
+    // holds this layout's zeros (the same shard rendered into it before) is not cleared again.
+    // Only ctx[0]'s block is output: the other devices of the process send their tiles to it.
+    // Their (index, count) = (shardIndex, shardCount·N) identify the process's layout, since N
+    // is fixed per Device (the debug renderer, which renders on ctx[0] alone, resets the key).
     if (memcmp(B.zeroKey, zkey, sizeof(zkey)) != 0) {
       HIP_CHECK(hipMemsetAsync(B.fbFloat.p, 0, (size_t)nf * W * H * 3 * sizeof(float), stream));
       HIP_CHECK(hipMemsetAsync(B.fbRGB8.p, 0, (size_t)nf * rgb8Stride * H, stream));

@@ -205,7 +205,13 @@ int yrtMain(int argc, const char** argv) {
   return rc ? 1 : 0;
 }
 
+}  // extern "C"
+
 // ====================================================================== DLL API
+// The entry points are declared extern "C" inside namespace Yulio (include/YulioRT.h), so these
+// definitions keep C linkage: the exported symbols are the plain names.
+namespace Yulio {
+
 static std::mutex g_trackerMu;
 static StatusRT g_status = {Inactive, 0.f, NoError};
 static std::atomic<bool> g_running{false}, g_stop{false};
@@ -361,4 +367,4 @@ void GetCurrentStatusRT(StatusRT* status) {
   *status = g_status;
 }
 
-}  // extern "C"
+}  // namespace Yulio
