@@ -33,17 +33,6 @@ struct GpuNode {
 };
 static_assert(sizeof(GpuNode) == 128, "node is one 128-B line");
 
-// 8-wide node of the any-hit (shadow) traversal, collapsed from the 4-wide BVH
-// (bvh_build.cpp collapse_bvh8): the same plane layout for eight children, so an axis's near
-// (or far) planes are two 16-B loads; child references as in GpuNode (leaves index the same
-// GpuTri array). Two 128-B lines.
-struct GpuNode8 {
-  float lox[8], hix[8], loy[8], hiy[8], loz[8], hiz[8];
-  int32_t child[8];
-  int32_t pad[8];
-};
-static_assert(sizeof(GpuNode8) == 256, "8-wide node is two 128-B lines");
-
 struct GpuTri {
   float v0[4];  // xyz, w = global triangle id (bits)
   float e1[4];  // xyz, w = flags (bits): bit0 cullBackFaces

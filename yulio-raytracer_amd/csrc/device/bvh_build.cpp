@@ -492,98 +492,7 @@ struct Collapser {
   }
 };
 
-// 4-wide -> 8-wide: a node takes its 4-wide node's children and opens the inner child of
-// largest surface area while the node stays at most 8 wide (the BVH2 -> BVH4 rule of
-// Collapser, one level up).
-struct Collapser8 {
-  const std::vector<GpuNode>& in;
-  std::vector<GpuNode8> out;
-  std::vector<int> src;
-  int maxStack = 0;
-  explicit Collapser8(const std::vector<GpuNode>& n) : in(n) {}
-  struct Slot {
-    int node, slot;
-  };
-  int ref(const Slot& s) const { return in[s.node].child[s.slot]; }
-  float area(const Slot& s) const {
-    const GpuNode& g = in[s.node];
-    const float dx = g.hix[s.slot] - g.lox[s.slot], dy = g.hiy[s.slot] - g.loy[s.slot],
-                dz = g.hiz[s.slot] - g.loz[s.slot];
-    return dx * dy + dy * dz + dz * dx;
-  }
-  int valid(int node) const {
-    int m = 0;
-    for (int j = 0; j < 4; ++j) m += in[node].child[j] != -1;
-    return m;
-  }
-  int collapse(int n4, int stackAbove) {
-    std::vector<Slot> ch;
-    for (int j = 0; j < 4; ++j)
-      if (in[n4].child[j] != -1) ch.push_back(Slot{n4, j});
-    while (true) {
-      int best = -1;
-      float bestArea = -1.f;
-      for (int k = 0; k < (int)ch.size(); ++k) {
-        const int r = ref(ch[k]);
-        if ((r & 31) != 0) continue;  // a leaf
-        if ((int)ch.size() - 1 + valid(r >> 5) > 8) continue;
-        if (area(ch[k]) > bestArea) { bestArea = area(ch[k]); best = k; }
-      }
-      if (best < 0) break;
-      const int cn = ref(ch[best]) >> 5;
-      bool first = true;
-      for (int j = 0; j < 4; ++j) {
-        if (in[cn].child[j] == -1) continue;
-        if (first) ch[best] = Slot{cn, j};
-        else ch.push_back(Slot{cn, j});
-        first = false;
-      }
-    }
-    const int ni = (int)out.size();
-    out.emplace_back();
-    src.resize(out.size() * 8, -1);
-    const int k = (int)ch.size();
-    const int stackHere = stackAbove + (k - 1);
-    maxStack = std::max(maxStack, stackHere);
-    int refs[8];
-    for (int j = 0; j < k; ++j) {
-      const int r = ref(ch[j]);
-      refs[j] = (r & 31) == 0 ? collapse(r >> 5, stackHere) << 5 : r;
-    }
-    GpuNode8& g = out[ni];
-    memset(&g, 0, sizeof(g));
-    for (int j = 0; j < 8; ++j) {
-      // empty slots: inverted infinite boxes, culled by the ordered-plane test (as GpuNode)
-      const bool v = j < k;
-      const GpuNode* s = v ? &in[ch[j].node] : nullptr;
-      const int q = v ? ch[j].slot : 0;
-      g.lox[j] = v ? s->lox[q] : INFINITY; g.hix[j] = v ? s->hix[q] : -INFINITY;
-      g.loy[j] = v ? s->loy[q] : INFINITY; g.hiy[j] = v ? s->hiy[q] : -INFINITY;
-      g.loz[j] = v ? s->loz[q] : INFINITY; g.hiz[j] = v ? s->hiz[q] : -INFINITY;
-      g.child[j] = v ? refs[j] : -1;
-      src[(size_t)ni * 8 + j] = v ? (ch[j].node << 2 | ch[j].slot) : -1;
-    }
-    return ni;
-  }
-};
-
 }  // namespace
-
-bool collapse_bvh8(const std::vector<GpuNode>& nodes4, int stackDepth, std::vector<GpuNode8>& nodes8,
-                   std::vector<int>& src, int& maxStack) {
-  nodes8.clear();
-  src.clear();
-  maxStack = 0;
-  if (nodes4.empty()) return false;
-  Collapser8 C(nodes4);
-  C.collapse(0, 0);
-  maxStack = C.maxStack;
-  // 8-wide node byte offsets (index << 8) must fit 32 bits (kernels/yrt_traverse.h node8_load)
-  if (C.maxStack > stackDepth - 1 || C.out.size() >= (size_t(1) << 24)) return false;
-  nodes8 = std::move(C.out);
-  src = std::move(C.src);
-  return true;
-}
 
 void build_bvh(const std::vector<float>& v /* 9 floats per triangle */, const std::vector<uint32_t>& flags,
                int stackDepth, BvhResult& out, const std::vector<float>* v1) {

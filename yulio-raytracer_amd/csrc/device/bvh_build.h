@@ -22,12 +22,5 @@ struct BvhResult {
 void build_bvh(const std::vector<float>& v, const std::vector<uint32_t>& flags, int stackDepth, BvhResult& out,
                const std::vector<float>* v1 = nullptr);
 
-// The any-hit traversal's 8-wide BVH over the same leaves: every 4-wide node whose children
-// (opened largest-area first while at most 8) become one 8-wide node's. src[8 n + s] is the
-// 4-wide (node << 2 | slot) whose box child s of 8-wide node n carries (-1: empty slot), so a
-// refit of the 4-wide BVH refits this one by copying planes (k_refit_nodes8). Returns false
-// (and leaves the outputs empty) when its worst-case stack exceeds stackDepth - 1.
-bool collapse_bvh8(const std::vector<GpuNode>& nodes4, int stackDepth, std::vector<GpuNode8>& nodes8,
-                   std::vector<int>& src, int& maxStack);
 
 }  // namespace yrt

@@ -52,23 +52,24 @@ struct GpuCtx {
   // latency-bound shading).
   struct Lane {
     hipStream_t stream = nullptr;
-    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, sIdx, counters, spill;
+    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
     int64_t pathCap = 0, shadowCap = 0;
     // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
     // copy of the counters (written by the stream after the batch's last trace), the event
-    // after that copy, the batch's tiles (progress) and its tiles per frame (grid-size hints).
-    // The host enqueues up to kPendDepth batches per lane ahead of the GPU, so the next batch's
-    // launches are queued before the lane finishes the previous one.
+    // after that copy, the batch's tiles (progress) and its place in the job (seq). A lane
+    // takes its next batch once its previous batch's counters have arrived — before that
+    // batch's pixel resolve, so the host enqueues while the resolve runs. Two batches ahead
+    // per lane measured the same (profiles/r04/ab_r04k.txt).
     struct Pend {
       unsigned* hc = nullptr;
       size_t hcWords = 0;
       hipEvent_t done = nullptr;
       int64_t tiles = 0;
-      std::vector<int64_t> frameTiles;
+      int64_t seq = 0;
       bool fused = false;  // depth 0 ran as k_trace's camera-ray instantiation
     };
-    static constexpr int kPendDepth = 2;
+    static constexpr int kPendDepth = 1;
     Pend pend[kPendDepth];
     int pendHead = 0, pendCount = 0;
   };
@@ -158,7 +159,6 @@ struct GpuCtx {
       L.sDir.alloc(S * 16);
       L.sContrib.alloc(S * 16);
       L.sOcc.alloc(S * 4);
-      if (shadow_origin_index_built()) L.sIdx.alloc(S * 4);
       L.shadowCap = S;
     }
     if (motion) {
@@ -456,11 +456,10 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
   // written (rank 0's framebuffers receive the gathered frames). A framebuffer with its own
   // host pixels keeps a reference to the frame in HBM instead, read back by rtMapFrameBuffer
   // (the reference's only access to the pixels, singleray_device.cpp:439-447): frames nobody
-  // maps cross no PCIe. YRT_EAGER_READBACK=1: copy at the end of every render.
+  // maps cross no PCIe.
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   const size_t rgb8Stride = ((size_t)3 * W + 3) / 4 * 4;
-  static const bool eager = getenv("YRT_EAGER_READBACK") != nullptr;
   for (int k = 0; k < nf && !(procGather && shardIndex != 0); ++k) {
     FrameBufferObj& Fk = *F[k];
     FrameBufferObj::Pending pf;
@@ -470,7 +469,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     pf.hipDevice = g0.hipDevice;
     if ((int)Fk.pending.size() < Fk.depth) Fk.pending.resize(Fk.depth);
     Fk.pending[Fk.cur] = pf;
-    if (eager || !Fk.userPtrs.empty()) fb_read_back(Fk, Fk.cur);
+    if (!Fk.userPtrs.empty()) fb_read_back(Fk, Fk.cur);
   }
   stats.samples = ctx[0]->stats.samples;
   stats.gather = gatherPath;
@@ -695,24 +694,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       }
       L.pendHead = L.pendCount = 0;
     }
-    // batches a lane may have enqueued ahead of the GPU (YRT_PEND_DEPTH, default 1: wait for
-    // the lane's previous batch — whose counters arrive before its pixel resolve — before
-    // enqueueing the next). Two ahead measured equal with full grids (profiles/r04/ab_r04k.txt)
-    const bool laneRoundRobin = getenv("YRT_LANE_ORDER") && strcmp(getenv("YRT_LANE_ORDER"), "rr") == 0;
-    const int pendDepth =
-        std::max(1, std::min(GpuCtx::Lane::kPendDepth, getenv("YRT_PEND_DEPTH") ? atoi(getenv("YRT_PEND_DEPTH")) : 1));
     // the other lanes start after the frame setup enqueued on lane 0 (uploads, pixel sets)
     if (nl > 1) {
       hipEvent_t setup = g.ev();
       HIP_CHECK(hipEventRecord(setup, stream));
       for (int l = 1; l < nl; ++l) HIP_CHECK(hipStreamWaitEvent(g.lanes[l].stream, setup, 0));
     }
-    // YRT_SHADOW_ORG_IDX=1 (kernels built with -DYRT_SHADOW_ORG_IDX=1): shadow rays read their
-    // origin from their vertex's continuation record (PathBuffers::sIdx) instead of carrying
-    // their own. Off: k_shade -2 % but the any-hit kernel's dependent origin load +2.5 %,
-    // frame -0.3 % (profiles/r04/ab_r04a.txt)
-    static const bool shadowOrgIdx =
-        shadow_origin_index_built() && getenv("YRT_SHADOW_ORG_IDX") && atoi(getenv("YRT_SHADOW_ORG_IDX")) != 0;
     auto lane_buffers = [&](GpuCtx::Lane& L) {
       PathBuffers pb;
       for (int k = 0; k < 2; ++k) {
@@ -728,8 +715,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.sDir = L.sDir.as<float4>();
       pb.sContrib = L.sContrib.as<float4>();
       pb.sOcc = L.sOcc.as<int>();
-      // the capture frame (roofline accounting) copies whole shadow records: own origins there
-      pb.sIdx = shadowOrgIdx && captureMax == 0 ? L.sIdx.as<int>() : nullptr;
       pb.counters = L.counters.as<unsigned>();
       for (int k = 0; k < 2; ++k) pb.qTime[k] = G.hasMotion ? L.qTime[k].as<float>() : nullptr;
       pb.sTime = G.hasMotion ? L.sTime.as<float>() : nullptr;
@@ -740,41 +725,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       pb.fuseShadow = numDirect == 1 && !getenv("YRT_NO_SHADOW_FUSE");
       return pb;
     };
-    // grid-size hints (YRT_GRID_HINTS=1; off by default): queue entries per tile of the drained
-    // batches, per frame and depth; a batch's hint is the sum over its frames of rate x tiles
-    // (-1 = a frame without a rate yet, full grids). Off: every launch gets the full grid (its
-    // waves grid-stride over the device-side count and idle ones exit at once). Round 4 measured
-    // the hints a loss: a band of a face inherits the previous band's rates (sky above, floor
-    // below), so grids come out too small; without them C4 runs 389 -> 371 ms on one GPU and
-    // its N = 2 / 3 rank shares 215 -> 189 / 162 -> 128 ms, C3 and N = 8 unchanged, and larger
-    // pads converge to the same (profiles/r04/ab_r04j.txt)
-    const bool useHints = getenv("YRT_GRID_HINTS") && atoi(getenv("YRT_GRID_HINTS")) != 0;
-    std::vector<double> rateC((size_t)nf * levels, -1.0), rateS((size_t)nf * levels, -1.0);
-    // YRT_HINT_MODE=max: a batch's hint is the highest rate per tile any drained batch of the
-    // job had at that depth, times its tiles (never below a band of the frame seen before)
-    const bool hintMax = getenv("YRT_HINT_MODE") && strcmp(getenv("YRT_HINT_MODE"), "max") == 0;
-    std::vector<double> maxRateC(levels, -1.0), maxRateS(levels, -1.0);
-    // the batch's tiles per frame: shard tile j of the batch is job tile index + j * count
-    auto frame_tiles = [&](int64_t firstTile, int64_t ntiles, int64_t* per) {
-      for (int f = 0; f < nf; ++f) per[f] = 0;
-      const int64_t tpf = rp.tilesPerFrame;
-      int64_t j = firstTile;
-      const int64_t jEnd = firstTile + ntiles;
-      while (j < jEnd) {
-        const int64_t f = (index + j * count) / tpf;
-        // last j whose tile is still in frame f: index + j * count < (f + 1) * tpf
-        int64_t jLast = ((f + 1) * tpf - 1 - index) / count;
-        if (jLast >= jEnd) jLast = jEnd - 1;
-        per[f] += jLast - j + 1;
-        j = jLast + 1;
-      }
-    };
-    std::vector<int64_t> curTiles(nf);
-    std::vector<long long> estClosest(levels, -1), estShadow(levels, -1);
-    // a launch's grid covers 1.5x the estimate plus a pad (the kernels grid-stride over the
-    // device-side count, so a short estimate costs time, never correctness); YRT_HINT_PAD
-    static const long long hintPad = getenv("YRT_HINT_PAD") ? atoll(getenv("YRT_HINT_PAD")) : 65536;
-    auto hint = [&](long long est) { return (!useHints || est < 0) ? -1ll : est + est / 2 + hintPad; };
     auto mit = g.missFrac.find(G.serial);
     double missEst = mit == g.missFrac.end() ? -1.0 : mit->second.first / mit->second.second;
     // accounts the queue counters of the lane's oldest pending batch; without `wait` only if
@@ -796,14 +746,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           nc += Pd.hc[qcounter_index(d, 0, k)];
           ns += Pd.hc[qcounter_index(d, 1, k)];
         }
-        // the batch's rate per tile, credited to each of its frames
-        for (int f = 0; f < nf; ++f)
-          if (Pd.frameTiles[f]) {
-            rateC[(size_t)f * levels + d] = nc / (double)Pd.tiles;
-            rateS[(size_t)f * levels + d] = ns / (double)Pd.tiles;
-          }
-        maxRateC[d] = std::max(maxRateC[d], nc / (double)Pd.tiles);
-        maxRateS[d] = std::max(maxRateS[d], ns / (double)Pd.tiles);
         if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
           if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
           auto& acc = g.missFrac[G.serial];
@@ -853,40 +795,27 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       missL.y = missL.y + 1.0f * Le[1];
       missL.z = missL.z + 1.0f * Le[2];
     }
-    // batch boundaries (first tile of each batch, then shardTiles). YRT_TAPER=1: the last round of
-    // batches (one per lane) is cut into twice as many half batches, so the lanes' final depth
-    // tails are shorter and end closer together
-    std::vector<int64_t> bounds;
-    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch) bounds.push_back(first);
-    const bool taper = getenv("YRT_TAPER") && atoi(getenv("YRT_TAPER")) != 0;
-    if (taper && nl > 1 && (int64_t)bounds.size() >= 2 * nl) {
-      const int64_t lastRound = bounds[bounds.size() - nl];
-      bounds.resize(bounds.size() - nl);
-      const int64_t rest = shardTiles - lastRound, pieces = 2 * nl, per = (rest + pieces - 1) / pieces;
-      for (int64_t f = lastRound; f < shardTiles; f += per) bounds.push_back(f);
-    }
-    bounds.push_back(shardTiles);
-    for (size_t bix = 0; bix + 1 < bounds.size(); ++bix, ++batch) {
-      const int64_t first = bounds[bix], batchTiles = bounds[bix + 1] - first;
+    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
+      const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - first);
       if (R.stopFlag && R.stopFlag->load()) break;
-      // the batch goes to the first lane with room in its ring (the fewest pending batches):
-      // finished batches are accounted as they arrive, on any lane, so a lane that finishes
-      // early is refilled at once instead of waiting for the other lane's older batch
-      // (round-robin lanes with one batch ahead: C4 N = 3 rank share 160 ms, YRT_LANE_ORDER=rr)
+      // the batch goes to the first lane with room in its ring: finished batches are accounted
+      // as they arrive, on any lane, so a lane that finishes early is refilled at once instead
+      // of waiting for the other lane's older batch (lanes in turn: C4 N = 3 rank share 160 ms,
+      // profiles/r04/ab_r04i.txt). When every ring is full the host blocks on the batch enqueued
+      // first (hipEventSynchronize) instead of spinning a core.
       int li = -1;
       for (;;) {
         for (int l = 0; l < nl; ++l)
           while (drain_one(g.lanes[l], false)) {}
-        if (laneRoundRobin) {
-          GpuCtx::Lane& R0 = g.lanes[batch % nl];
-          if (R0.pendCount < pendDepth) { li = (int)(batch % nl); break; }
-          drain_one(R0, true);
-          continue;
-        }
         for (int l = 0; l < nl; ++l)
-          if (g.lanes[l].pendCount < pendDepth && (li < 0 || g.lanes[l].pendCount < g.lanes[li].pendCount)) li = l;
+          if (g.lanes[l].pendCount < GpuCtx::Lane::kPendDepth &&
+              (li < 0 || g.lanes[l].pendCount < g.lanes[li].pendCount))
+            li = l;
         if (li >= 0) break;
-        std::this_thread::yield();
+        int oldest = 0;
+        for (int l = 1; l < nl; ++l)
+          if (g.lanes[l].pend[g.lanes[l].pendHead].seq < g.lanes[oldest].pend[g.lanes[oldest].pendHead].seq) oldest = l;
+        drain_one(g.lanes[oldest], true);
       }
       GpuCtx::Lane& L = g.lanes[li];
       const hipStream_t st = L.stream;
@@ -899,24 +828,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.tileStride = count;
       bi.tileOffset = index;
       bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
-      frame_tiles(first, bi.numPixels / 256, curTiles.data());
-      for (int d = 0; d < levels; ++d) {
-        double ec = 0, es = 0;
-        bool known = true;
-        for (int f = 0; f < nf && known; ++f) {
-          if (!curTiles[f]) continue;
-          const double rc = rateC[(size_t)f * levels + d], rs = rateS[(size_t)f * levels + d];
-          known = rc >= 0;
-          ec += rc * (double)curTiles[f];
-          es += rs * (double)curTiles[f];
-        }
-        estClosest[d] = known ? (long long)ec : -1;
-        estShadow[d] = known ? (long long)es : -1;
-        if (hintMax) {
-          estClosest[d] = maxRateC[d] >= 0 ? (long long)(maxRateC[d] * (double)batchTiles) : -1;
-          estShadow[d] = maxRateS[d] >= 0 ? (long long)(maxRateS[d] * (double)batchTiles) : -1;
-        }
-      }
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
       // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
       // YRT_PRIMARY_IDENTITY=1 for the scenes whose rays mostly hit) or k_raygen otherwise
@@ -946,7 +857,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           launch_trace_primary(lsv, pr, pb.hit, st);
         } else {
           launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                               pb.segCap, pb.hit, st, hint(estClosest[d]), pb.qTime[cur]);
+                               pb.segCap, pb.hit, st, pb.qTime[cur]);
         }
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && first == 0)
@@ -954,19 +865,19 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                     pb.segCap, st);
         EvPair e2{};
         if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
-        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st, hint(estClosest[d]));
+        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (numDirect > 0) {
           EvPair e3{};
           if (kernelTiming) { e3 = {g.ev(), g.ev(), 1}; HIP_CHECK(hipEventRecord(e3.a, st)); }
-          const ShadowFuse sf{pb.fuseShadow ? pb.sContrib : nullptr, pb.pathL, pb.sIdx, pb.qOrg[cur ^ 1]};
+          const ShadowFuse sf{pb.fuseShadow ? pb.sContrib : nullptr, pb.pathL};
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
-                           pb.sOcc, st, &sf, hint(estShadow[d]), pb.sTime);
+                           pb.sOcc, st, &sf, pb.sTime);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
           if (captureMax > 0 && first == 0)
             g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),
                       pb.shSegCap, st);
-          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st, hint(estClosest[d]));
+          if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st);
         }
       }
       // the counters are final after the last trace: their copy runs before the pixel resolve,
@@ -976,7 +887,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipEventRecord(Pd.done, st));
       Pd.tiles = bi.numPixels / 256;
       Pd.fused = fusedBatch;
-      Pd.frameTiles.assign(curTiles.begin(), curTiles.end());
+      Pd.seq = batch;
       L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,
                             g.dAccu.as<float4>(), accumulate ? 1 : 0, st);

@@ -17,17 +17,9 @@
 namespace yrt {
 
 // SceneView pointers of the scene's own device buffers (counts already set in S.view)
-// YRT_ANY_BVH8=1: the any-hit kernel traverses an 8-wide BVH collapsed from the 4-wide one
-// (off by default: C3 shadow trace +31 % per launch).
-static bool any_bvh8_enabled() {
-  const char* e = getenv("YRT_ANY_BVH8");
-  return e && atoi(e) != 0;
-}
-
 static void bind_view(GpuScene& S) {
   SceneView& v = S.view;
   v.nodes = S.nodes.as<GpuNode>();
-  v.nodes8 = S.nodes8.as<GpuNode8>();
   v.tris = S.tris.as<GpuTri>();
   v.triGeom = S.triGeom.as<int>();
   v.indices = S.indices.as<int4>();
@@ -310,15 +302,6 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   for (const GpuMaterial& m : materials) S->materialMask |= 1u << m.type;
   for (const GpuLight& l : lights) S->materialMask |= 1u << (16 + l.type);  // light_bit (kernels/yrt_shade.h)
   S->nodes.upload(bvh.nodes);
-  if (any_bvh8_enabled()) {
-    std::vector<GpuNode8> n8;
-    std::vector<int> src8;
-    if (collapse_bvh8(bvh.nodes, stackDepth, n8, src8, S->bvh8Depth)) {
-      S->nodes8.upload(n8);
-      S->nodes8Src.upload(src8);
-      S->numNodes8 = (int)n8.size();
-    }
-  }
   S->tris.upload(bvh.tris);
   S->triGeom.upload(triGeom);
   S->indices.upload(indices);
@@ -477,10 +460,6 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
     HIP_CHECK(hipMemcpyPeer(dst.p, device, from.p, src.device, from.bytes));
   };
   copy(R->nodes, src.nodes);
-  copy(R->nodes8, src.nodes8);
-  copy(R->nodes8Src, src.nodes8Src);
-  R->numNodes8 = src.numNodes8;
-  R->bvh8Depth = src.bvh8Depth;
   copy(R->tris, src.tris);
   copy(R->triGeom, src.triGeom);
   copy(R->indices, src.indices);
@@ -566,9 +545,6 @@ bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>&
   for (int d = (int)S.levelStart.size() - 2; d >= 0; --d)
     launch_refit_nodes(S.nodes.as<GpuNode>(), S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(),
                        S.levelNodes.as<int>() + S.levelStart[d], S.levelStart[d + 1] - S.levelStart[d], stream);
-  // the 8-wide nodes take their children's boxes from the refit 4-wide nodes
-  if (S.numNodes8)
-    launch_refit_nodes8(S.nodes8.as<GpuNode8>(), S.nodes.as<GpuNode>(), S.nodes8Src.as<int>(), S.numNodes8, stream);
   HIP_CHECK(hipStreamSynchronize(stream));
   S.hostBvhStale = true;
   S.refits++;

@@ -60,10 +60,6 @@ struct GpuScene {
   }
   DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
       lights, envLights, hdriDist, media, geomRecs, motions, tangents, triMotion, triShade;
-  // the any-hit traversal's 8-wide BVH over the same leaves (bvh_build.h collapse_bvh8; empty
-  // when disabled, YRT_ANY_BVH8=0, or over the stack bound): nodes8 and its 4-wide sources
-  DevBuf nodes8, nodes8Src;
-  int numNodes8 = 0, bvh8Depth = 0;
   bool hasMotion = false;  // moving geometry: time-aware trace kernels, no refit
   SceneView view{};
   unsigned materialMask = 0;  // bit MAT_x per material type, bit 16+LIGHT_x per light type used (shade kernel variant)

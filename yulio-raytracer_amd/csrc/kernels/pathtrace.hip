@@ -402,21 +402,6 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS_ANY
 #define YRT_NODE_BIAS_ANY 12  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %
 #endif
-#ifndef YRT_SHADOW_ORG_IDX
-// 1: a shadow ray may read its origin from its vertex's continuation record (PathBuffers::sIdx,
-// enabled at run time by YRT_SHADOW_ORG_IDX=1). Compiled out by default: k_shade -2 % but the
-// any-hit refill's dependent origin load +2.5 %, frame -0.3 % (profiles/r04/ab_r04a.txt), and
-// the runtime branch held registers in both kernels (k_shade scratch spills on C4)
-#define YRT_SHADOW_ORG_IDX 0
-#endif
-#ifndef YRT_SHADE_PAIR_APPEND
-// 1: with one light, the continuation and shadow slots by one 64-bit atomic per wave instead of
-// two 32-bit ones. Off: C3 k_shade -2.2 % but frame +0.3 % within the spread
-// (profiles/r04/ab_r04a.txt), and the light term then runs with the continuation's records
-// live: C4's MetallicPaint kernel spills 37 VGPRs to scratch and its cubemap runs 4.5 % slower
-// (profiles/r04/bisect_r04.txt)
-#define YRT_SHADE_PAIR_APPEND 0
-#endif
 #ifndef YRT_NODE_UNROLL_ANY
 #define YRT_NODE_UNROLL_ANY 1  // any-hit: node steps between two node/leaf-phase checks
 #endif
@@ -469,13 +454,11 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 
 // MOTION: moving geometry; rayTime[q] is query q's time (Ray::time, set from sample.getTime()
 // for camera rays and inherited by shadow and continuation rays, pathtraceintegrator.cpp:158,210)
-// WIDE (any-hit only): node steps on the 8-wide BVH (sv.nodes8, GpuNode8): the farthest hit
-// child next, the other hit ones pushed — fewer, wider steps per query
 // PRIM (closest hit, static scenes): depth 0 from the batch's path ids instead of a queue —
 // camera rays generated at refill, hits appended to the depth-0 queue, misses resolved
 // (PrimaryRays); 1 / 3: pinhole cameras only (the other cameras' code would cost registers),
 // 2 / 4: any camera; 3 / 4: identity layout (PrimaryRays::identity), 1 / 2: hits compacted
-template <bool ANY, bool MOTION, bool WIDE = false, int PRIM = 0>
+template <bool ANY, bool MOTION, int PRIM = 0>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(
     ANY ? YRT_TRACE_WAVES_ANY : PRIM ? YRT_TRACE_WAVES_PRIM : YRT_TRACE_WAVES))) void k_trace(
     SceneView sv, const float4* __restrict__ org,
@@ -485,7 +468,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          int* __restrict__ occOut, int* __restrict__ spillBuf,
                                                          ShadowFuse sf, const float* __restrict__ rayTime,
                                                          PrimaryRays pr) {
-  static_assert(!PRIM || (!ANY && !MOTION && !WIDE), "camera rays: closest hit, static scenes");
+  static_assert(!PRIM || (!ANY && !MOTION), "camera rays: closest hit, static scenes");
   constexpr bool kPinhole = PRIM == 1 || PRIM == 3, kIdentity = PRIM >= 3;
   constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
   __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
@@ -671,17 +654,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
               }
             } else {
             q = qmap_phys(qm, segCap, li);
-#if YRT_SHADOW_ORG_IDX
-            if (ANY && sf.orgIdx) {
-              // a shadow ray shares its origin record with its vertex's continuation ray
-              const int oi = sf.orgIdx[q];
-              ro = oi >= 0 ? sf.orgCont[oi] : org[q];
-            } else {
-              ro = org[q];
-            }
-#else
             ro = org[q];
-#endif
             rd = dir[q];
             if (MOTION) rtime = rayTime[q];
             }
@@ -760,33 +733,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       YRT_PROF(2, 1);
       YRT_PROF(3, __popcll(ballot(has && curCnt == 0)));
       if (has && curCnt == 0) {
-       if constexpr (WIDE) {
-        float t[8];
-        int c[8];
-        box8_any(sv.nodes8, curIdx, __float_as_int(ri.w), r, best.t, t, c);
-        far8(t, c);
-        const float MISS = __int_as_float(0xff800000);
-        if (sp + 7 <= kLds) {
-          // unconditional stores into free ring slots, sp advanced past the hit ones (as below)
-          int o = sp;
-#pragma unroll
-          for (int k = 7; k >= 1; --k) {
-            stack[YRT_SLOT(o)] = c[k];
-            o += t[k] > MISS ? 1 : 0;
-          }
-          sp = o;
-        } else {
-#pragma unroll
-          for (int k = 7; k >= 1; --k)
-            if (t[k] > MISS) YRT_PUSH(c[k]);
-        }
-        if (t[0] > MISS) {
-          curIdx = c[0] >> 5;
-          curCnt = c[0] & 31;
-        } else {
-          YRT_POP();
-        }
-       } else {
         float t[4];
         int c[4];
         // sign-ordered slab planes (+1.5 % on C3 with two lanes, bit-identical distances)
@@ -819,7 +765,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
           YRT_POP();
         }
 #undef YRT_HIT
-       }
         if (curCnt > 0 && pendCnt == 0) {
           pendIdx = curIdx;
           pendCnt = curCnt;
@@ -1662,53 +1607,14 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       }
       return false;
     };
-    // shadow ray records at slot si; its origin (dg.P, dg.error * epsilon) is the continuation's
-    // (queue slot nq) when there is one
-    auto shadow_store = [&](unsigned si, const V3& wi, float tfar, const V3& contrib, bool withCont, unsigned nq) {
+    // shadow ray records at slot si: origin (dg.P, dg.error * epsilon), direction and tfar, the
+    // light's contribution and the path id
+    auto shadow_store = [&](unsigned si, const V3& wi, float tfar, const V3& contrib) {
       if (pb.sTime) pb.sTime[si] = samp(fv, 4, rec);  // lastRay.time (:158)
-#if YRT_SHADOW_ORG_IDX
-      if (pb.sIdx) pb.sIdx[si] = withCont ? (int)nq : -1;
-      if (!pb.sIdx || !withCont) pb.sOrg[si] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
-#else
-      (void)withCont;
-      (void)nq;
       pb.sOrg[si] = make_float4(dg.P.x, dg.P.y, dg.P.z, dg.error * rp.epsilon);
-#endif
       pb.sDir[si] = make_float4(wi.x, wi.y, wi.z, tfar);
       pb.sContrib[si] = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(path));
     };
-#if YRT_SHADE_PAIR_APPEND
-    if (numDirect == 1) {
-      // one light: the shadow ray and the continuation take their queue slots with ONE 64-bit
-      // atomic per wave on the segment's counter pair (shadow count of this depth in the low
-      // word, continuation count of the next in the high word, qcounter_index)
-      V3 wi = v3s(0.f), contrib = v3s(0.f);
-      float tfar = 0.f;
-      const bool pred = light_term(0, wi, tfar, contrib);
-      SPROF_FINE(5);  // shadow-ray jitter, contribution
-      const unsigned long long mc = ballot(cont), ms = ballot(pred);
-      unsigned bc = 0, bsh = 0;
-      if (mc | ms) {
-        const int lane = lane_id();
-        const int leader = __ffsll((long long)(mc | ms)) - 1;
-        unsigned long long old = 0;
-        if (lane == leader)
-          old = atomicAdd((unsigned long long*)shadowCount,
-                          (unsigned long long)__popcll(ms) | ((unsigned long long)__popcll(mc) << 32));
-        const unsigned lo = __shfl((unsigned)old, leader, 64), hi = __shfl((unsigned)(old >> 32), leader, 64);
-        const unsigned long long lt = (1ull << lane) - 1ull;
-        bsh = lo + (unsigned)__popcll(ms & lt);
-        bc = hi + (unsigned)__popcll(mc & lt);
-      }
-      const unsigned nq = oseg * pb.segCap + bc;
-      const unsigned si = oseg * pb.shSegCap + bsh;
-      if (cont) cont_store(nq);
-      if (pred) shadow_store(si, wi, tfar, contrib, cont, nq);
-      if (active && !pb.fuseShadow) pb.shFirst[q] = pred ? (int)si : -1;
-      SPROF_MARK(5);
-      SPROF_FINE(6);
-    } else
-#endif
     {
       bool got;
       const unsigned nq = oseg * pb.segCap + wave_append(nextCount, cont, got);
@@ -1722,7 +1628,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
         SPROF_FINE(5);  // shadow-ray jitter, contribution
         bool sgot;
         const unsigned si = oseg * pb.shSegCap + wave_append(shadowCount, pred, sgot);
-        if (sgot) shadow_store(si, wi, tfar, contrib, got, nq);
+        if (sgot) shadow_store(si, wi, tfar, contrib);
         if (active && !pb.fuseShadow) pb.shFirst[(size_t)q * numDirect + k] = sgot ? (int)si : -1;
         SPROF_FINE(6);  // shadow-ray append and stores
       }
@@ -1920,14 +1826,9 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
   hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_RAYGEN_GRID)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
 }
 
-static inline long long hinted(long long maxCount, long long hint) {
-  return hint >= 0 && hint < maxCount ? hint : maxCount;
-}
-
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint, const float* time) {
-  const long long maxCount = hinted((long long)numSegs * segCap, countHint);
-  const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time) {
+  const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   if (time)
     hipLaunchKernelGGL((k_trace<false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
                        hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, time, PrimaryRays{});
@@ -1939,7 +1840,7 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
 #define YRT_LAUNCH_PRIM(k)                                                                                 \
-  hipLaunchKernelGGL((k_trace<false, false, false, k>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr, \
+  hipLaunchKernelGGL((k_trace<false, false, k>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr, \
                      (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,      \
                      ShadowFuse{}, (const float*)nullptr, pr)
   if (pr.identity) {
@@ -1952,30 +1853,16 @@ void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hi
 #undef YRT_LAUNCH_PRIM
 }
 
-bool shadow_origin_index_built() { return YRT_SHADOW_ORG_IDX != 0; }
-
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
-                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, long long countHint,
-                      const float* time) {
-  const long long maxCount = hinted((long long)numSegs * segCap, countHint);
-  const dim3 grid(grid_for(maxCount, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+                      int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, const float* time) {
+  const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   const ShadowFuse sf = fuse ? *fuse : ShadowFuse{};
-  // the 8-wide BVH when the scene has one (scene_gpu.cpp: YRT_ANY_BVH8, the stack bound)
-  if (time) {
-    if (sv.nodes8)
-      hipLaunchKernelGGL((k_trace<true, true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
-                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});
-    else
-      hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});
-  } else {
-    if (sv.nodes8)
-      hipLaunchKernelGGL((k_trace<true, false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts,
-                         numSegs, segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr, PrimaryRays{});
-    else
-      hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                         segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr, PrimaryRays{});
-  }
+  if (time)
+    hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                       segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});
+  else
+    hipLaunchKernelGGL((k_trace<true, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
+                       segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, (const float*)nullptr, PrimaryRays{});
 }
 
 // Instantiated material sets (bitmask of MAT_x): the launcher picks the smallest superset of
@@ -1997,17 +1884,17 @@ static const unsigned kShadeVariants[] = {YRT_SV_UBER,   YRT_SV_OBJ,     YRT_SV_
 
 template <unsigned MM>
 static void launch_shade_t(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi,
-                           int depth, hipStream_t s, long long countHint) {
+                           int depth, hipStream_t s) {
 #ifndef YRT_SHADE_GRID
 #define YRT_SHADE_GRID 16384  // blocks of YRT_BLOCK; swept 2048..32768 (x 256 and 64 lanes)
 #endif
-  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(hinted(pb.capacity, countHint), YRT_BLOCK, YRT_SHADE_GRID)),
+  hipLaunchKernelGGL(k_shade<MM>, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_SHADE_GRID)),
                      dim3(YRT_BLOCK), 0, s, sv, fv, pb,
                      bi, depth);
 }
 
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  unsigned materialMask, hipStream_t s, long long countHint) {
+                  unsigned materialMask, hipStream_t s) {
   unsigned pick = YRT_SV_ALL;
   for (unsigned v : kShadeVariants)
     if ((materialMask & ~v) == 0) {
@@ -2015,11 +1902,11 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
       break;
     }
   switch (pick) {
-    case YRT_SV_UBER: launch_shade_t<YRT_SV_UBER>(sv, fv, pb, bi, depth, s, countHint); break;
-    case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s, countHint); break;
-    case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s, countHint); break;
-    case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s, countHint); break;
-    case YRT_SV_COLLADA: launch_shade_t<YRT_SV_COLLADA>(sv, fv, pb, bi, depth, s, countHint); break;
+    case YRT_SV_UBER: launch_shade_t<YRT_SV_UBER>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_OBJ: launch_shade_t<YRT_SV_OBJ>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_SPHERES: launch_shade_t<YRT_SV_SPHERES>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_STEREO: launch_shade_t<YRT_SV_STEREO>(sv, fv, pb, bi, depth, s); break;
+    case YRT_SV_COLLADA: launch_shade_t<YRT_SV_COLLADA>(sv, fv, pb, bi, depth, s); break;
     default: {
       // the generic kernel (every material and light type) holds ~218 VGPRs, 2 waves/SIMD:
       // say so once per material set, so a scene outside the specialized sets is not slow
@@ -2034,14 +1921,14 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
                   "(2 waves/SIMD, slower shading)\n",
                   materialMask);
       }
-      launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s, countHint);
+      launch_shade_t<YRT_SV_ALL>(sv, fv, pb, bi, depth, s);
       break;
     }
   }
 }
 
-void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s, long long countHint) {
-  hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(hinted(pb.capacity, countHint), YRT_BLOCK, 8192)), dim3(YRT_BLOCK),
+void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {
+  hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK),
                      0, s, pb, depth,
                      numLights);
 }
@@ -2309,28 +2196,6 @@ void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices,
   if (count <= 0) return;
   hipLaunchKernelGGL(k_refit_nodes, dim3((count + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes, tris,
                      indices, positions, levelNodes, count);
-}
-
-// the 8-wide any-hit BVH after a 4-wide refit: every child box is a 4-wide node's child box
-__global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes8(GpuNode8* __restrict__ nodes8,
-                                                           const GpuNode* __restrict__ nodes,
-                                                           const int* __restrict__ src, int count) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count * 8) return;
-  const int s = src[i];
-  if (s < 0) return;  // empty slot: its inverted box stays
-  const GpuNode& n = nodes[s >> 2];
-  const int q = s & 3, j = i & 7;
-  GpuNode8& o = nodes8[i >> 3];
-  o.lox[j] = n.lox[q]; o.hix[j] = n.hix[q];
-  o.loy[j] = n.loy[q]; o.hiy[j] = n.hiy[q];
-  o.loz[j] = n.loz[q]; o.hiz[j] = n.hiz[q];
-}
-
-void launch_refit_nodes8(GpuNode8* nodes8, const GpuNode* nodes, const int* src, int numNodes8, hipStream_t s) {
-  if (numNodes8 <= 0) return;
-  hipLaunchKernelGGL(k_refit_nodes8, dim3((numNodes8 * 8 + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes8,
-                     nodes, src, numNodes8);
 }
 
 }  // namespace yrt

@@ -12,7 +12,6 @@ namespace yrt {
 
 struct SceneView {
   const GpuNode* nodes;
-  const GpuNode8* nodes8;  // the any-hit traversal's 8-wide BVH (null: any-hit uses nodes)
   const GpuTri* tris;
   const int* triGeom;
   const int4* indices;
@@ -73,7 +72,7 @@ struct FrameView {
 // counters[((level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE], kind 0 = closest queue
 // entering depth `level`, kind 1 = shadow rays emitted at depth `level`; except that the
 // closest queue entering depth level > 0 counts in the word after the shadow counter of depth
-// level - 1 (same segment): k_shade appends both with one 64-bit atomic (one light).
+// level - 1 (same segment).
 inline __host__ __device__ size_t qcounter_index(int level, int kind, int seg) {
   if (kind == 0 && level > 0) return ((size_t)((level - 1) * 2 + 1) * YRT_QSEGS + seg) * YRT_QCSTRIDE + 1;
   return ((size_t)(level * 2 + kind) * YRT_QSEGS + seg) * YRT_QCSTRIDE;
@@ -98,11 +97,7 @@ struct PathBuffers {
   float4* pathL;     // per path id: radiance so far (emission and unoccluded direct light are
                      // read-modify-written in the reference's order; one writer per path at a time)
   int* shFirst;      // per (queue slot, light): shadow-ray slot or -1
-  float4* sOrg;      // shadow rays (the origin only where sIdx is -1, see sIdx)
-  // per shadow slot: the continuation-queue slot (qOrg[cur ^ 1]) holding the shadow ray's
-  // origin — the same (P, error * epsilon) as the continuation's (pathtraceintegrator.cpp:
-  // 158,210), written once — or -1 (no continuation: the origin is in sOrg). null: sOrg always.
-  int* sIdx;
+  float4* sOrg;      // shadow rays: origin xyz, tnear
   float4* sDir;
   float4* sContrib;
   int* sOcc;
@@ -123,8 +118,6 @@ struct PathBuffers {
 struct ShadowFuse {
   const float4* contrib;  // null: not fused, k_trace<true> writes occlusion flags
   float4* pathL;
-  const int* orgIdx;      // PathBuffers::sIdx (null: the origins are the org array's)
-  const float4* orgCont;  // the continuation queue's origins that orgIdx indexes
 };
 
 struct BatchInfo {
@@ -135,7 +128,7 @@ struct BatchInfo {
   FastDiv divPixels;   // fastdiv_make(numPixels): path id -> (sample, batch pixel)
 };
 
-// Camera rays generated inside the closest-hit kernel (k_trace<false, false, false, true>):
+// Camera rays generated inside the closest-hit kernel (k_trace<false, false, PRIM>):
 // depth 0 without a raygen pass. A lane takes the batch's next path id, computes its camera ray
 // as k_raygen does, traces it and, when it is done, either appends it with its hit to the
 // depth-0 queue (qPath/qOrg/qDir/hit, the segment of its path id's 64-group) or, on a miss,
@@ -166,26 +159,23 @@ void launch_pixel_sets(const FrameView& fv, uint8_t* pixelSets, int width, int h
 void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, hipStream_t s);
 // counts: first segment counter of the queue (segments YRT_QCSTRIDE apart), numSegs segments
 // of segCap slots; hit/occluded are indexed by physical slot.
-// countHint (>= 0): expected queue length, sizes the grid (the kernels grid-stride over the
-// real device-side count, so a low hint costs speed, never correctness); -1: full grid.
+// Every launch gets the full grid for the queue's capacity: the kernels grid-stride over the
+// device-side count and idle waves exit at once.
 // time (moving scenes): per-slot ray time (Ray::time); null: static scene (or time 0)
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, long long countHint = -1,
-                          const float* time = nullptr);
+                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time = nullptr);
 // depth 0 of a batch: camera rays generated, traced and queued (hits) or resolved (misses) in
 // one kernel, see PrimaryRays; replaces launch_raygen + the depth-0 launch_trace_closest for
 // static scenes without a backplate or direction-dependent environment lights
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s);
-// whether the kernels were built with the shared shadow-ray origins (-DYRT_SHADOW_ORG_IDX=1)
-bool shadow_origin_index_built();
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr,
-                      long long countHint = -1, const float* time = nullptr);
+                      const float* time = nullptr);
 // materialMask: bit MAT_x set for every material type the scene uses (selects a specialized
 // instantiation of the shade kernel)
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
-                  unsigned materialMask, hipStream_t s, long long countHint = -1);
-void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s, long long countHint = -1);
+                  unsigned materialMask, hipStream_t s);
+void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
@@ -219,8 +209,6 @@ void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices,
                        hipStream_t s);
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
                         const int* levelNodes, int count, hipStream_t s);
-// 8-wide nodes: child s of node n takes the box of 4-wide (src[8n+s] >> 2, src[8n+s] & 3)
-void launch_refit_nodes8(GpuNode8* nodes8, const GpuNode* nodes, const int* src, int numNodes8, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 

@@ -194,88 +194,6 @@ __device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, fl
 #undef YRT_CHILD
 }
 
-// Any-hit 8-wide node step (GpuNode8): the same slab test as box4_data for eight children,
-// with the sign-ordered planes of each axis at byte offsets 0 / 32 within the node's lo/hi
-// pair (planeOff << 1). Missed children (and empty slots: inverted infinite boxes) get -INF.
-__device__ __forceinline__ void box8_any(const GpuNode8* __restrict__ base, int nodeIdx, int planeOff, const RayPre& r,
-                                         float tmax, float t[8], int c[8]) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const char* b0 = (const char*)base;
-  const unsigned nb = (unsigned)nodeIdx << 8;
-  const unsigned ox = ((unsigned)planeOff & 0xffu) << 1, oy = (((unsigned)planeOff >> 8) & 0xffu) << 1,
-                 oz = ((unsigned)planeOff >> 16) << 1;
-#define YRT_L4(off) (*(const float4*)(b0 + (off)))
-  const float4 nxa = YRT_L4(nb + ox), nxb = YRT_L4(nb + ox + 16u);
-  const float4 fxa = YRT_L4(nb + (32u - ox)), fxb = YRT_L4(nb + (48u - ox));
-  const float4 nya = YRT_L4(nb + 64u + oy), nyb = YRT_L4(nb + 80u + oy);
-  const float4 fya = YRT_L4(nb + (96u - oy)), fyb = YRT_L4(nb + (112u - oy));
-  const float4 nza = YRT_L4(nb + 128u + oz), nzb = YRT_L4(nb + 144u + oz);
-  const float4 fza = YRT_L4(nb + (160u - oz)), fzb = YRT_L4(nb + (176u - oz));
-  const int4 cha = *(const int4*)(b0 + (nb + 192u)), chb = *(const int4*)(b0 + (nb + 208u));
-#undef YRT_L4
-  const f2 ix = {r.inv.x, r.inv.x}, iy = {r.inv.y, r.inv.y}, iz = {r.inv.z, r.inv.z};
-  const f2 mx = {-r.oi.x, -r.oi.x}, my = {-r.oi.y, -r.oi.y}, mz = {-r.oi.z, -r.oi.z};
-#define YRT_SLAB(P, I, M) __builtin_elementwise_fma(P, I, M)
-#define YRT_PAIR(V, a, b, I, M) YRT_SLAB((f2{V.a, V.b}), I, M)
-  const f2 nx[4] = {YRT_PAIR(nxa, x, y, ix, mx), YRT_PAIR(nxa, z, w, ix, mx), YRT_PAIR(nxb, x, y, ix, mx),
-                    YRT_PAIR(nxb, z, w, ix, mx)};
-  const f2 fx[4] = {YRT_PAIR(fxa, x, y, ix, mx), YRT_PAIR(fxa, z, w, ix, mx), YRT_PAIR(fxb, x, y, ix, mx),
-                    YRT_PAIR(fxb, z, w, ix, mx)};
-  const f2 ny[4] = {YRT_PAIR(nya, x, y, iy, my), YRT_PAIR(nya, z, w, iy, my), YRT_PAIR(nyb, x, y, iy, my),
-                    YRT_PAIR(nyb, z, w, iy, my)};
-  const f2 fy[4] = {YRT_PAIR(fya, x, y, iy, my), YRT_PAIR(fya, z, w, iy, my), YRT_PAIR(fyb, x, y, iy, my),
-                    YRT_PAIR(fyb, z, w, iy, my)};
-  const f2 nz[4] = {YRT_PAIR(nza, x, y, iz, mz), YRT_PAIR(nza, z, w, iz, mz), YRT_PAIR(nzb, x, y, iz, mz),
-                    YRT_PAIR(nzb, z, w, iz, mz)};
-  const f2 fz[4] = {YRT_PAIR(fza, x, y, iz, mz), YRT_PAIR(fza, z, w, iz, mz), YRT_PAIR(fzb, x, y, iz, mz),
-                    YRT_PAIR(fzb, z, w, iz, mz)};
-#undef YRT_PAIR
-#undef YRT_SLAB
-  const float MISS = __int_as_float(0xff800000);
-  // hardware min/max as in box4_data (no re-quieting of the loop-carried tnear / tmax)
-#define YRT_CHILD8(k, NX, FX, NY, FY, NZ, FZ, CH)                                           \
-  do {                                                                                      \
-    float nn, ff, a_, b_;                                                                   \
-    asm("v_max_f32 %0, %1, %2" : "=v"(a_) : "v"(NZ), "v"(r.tnear));                         \
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(nn) : "v"(NX), "v"(NY), "v"(a_));                \
-    asm("v_min_f32 %0, %1, %2" : "=v"(b_) : "v"(FZ), "v"(tmax));                            \
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(ff) : "v"(FX), "v"(FY), "v"(b_));                \
-    t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;                  \
-    c[k] = (CH);                                                                            \
-  } while (0)
-  YRT_CHILD8(0, nx[0].x, fx[0].x, ny[0].x, fy[0].x, nz[0].x, fz[0].x, cha.x);
-  YRT_CHILD8(1, nx[0].y, fx[0].y, ny[0].y, fy[0].y, nz[0].y, fz[0].y, cha.y);
-  YRT_CHILD8(2, nx[1].x, fx[1].x, ny[1].x, fy[1].x, nz[1].x, fz[1].x, cha.z);
-  YRT_CHILD8(3, nx[1].y, fx[1].y, ny[1].y, fy[1].y, nz[1].y, fz[1].y, cha.w);
-  YRT_CHILD8(4, nx[2].x, fx[2].x, ny[2].x, fy[2].x, nz[2].x, fz[2].x, chb.x);
-  YRT_CHILD8(5, nx[2].y, fx[2].y, ny[2].y, fy[2].y, nz[2].y, fz[2].y, chb.y);
-  YRT_CHILD8(6, nx[3].x, fx[3].x, ny[3].x, fy[3].x, nz[3].x, fz[3].x, chb.z);
-  YRT_CHILD8(7, nx[3].y, fx[3].y, ny[3].y, fy[3].y, nz[3].y, fz[3].y, chb.w);
-#undef YRT_CHILD8
-}
-
-// The farthest of eight (t, child) pairs to slot 0 (7 descending comparators: a max
-// tournament, the losers keep their slots' order); misses are -INF.
-__device__ __forceinline__ void far8(float t[8], int c[8]) {
-#define YRT_CSWAP_D(a, b)                        \
-  do {                                           \
-    const bool sw = t[b] > t[a];                 \
-    const float ta = sw ? t[b] : t[a];           \
-    const float tb = sw ? t[a] : t[b];           \
-    const int ca = sw ? c[b] : c[a];             \
-    const int cb = sw ? c[a] : c[b];             \
-    t[a] = ta; t[b] = tb; c[a] = ca; c[b] = cb;  \
-  } while (0)
-  YRT_CSWAP_D(0, 1);
-  YRT_CSWAP_D(2, 3);
-  YRT_CSWAP_D(4, 5);
-  YRT_CSWAP_D(6, 7);
-  YRT_CSWAP_D(0, 2);
-  YRT_CSWAP_D(4, 6);
-  YRT_CSWAP_D(0, 4);
-#undef YRT_CSWAP_D
-}
-
 // Sorts the four (t, child) pairs by t ascending (5-comparator network, stable for equal t).
 // (A 3-comparator nearest-first order saves 10 VALU per node step but visits 1.4 % more nodes:
 // -0.6 % on C3, profiles/r02/trace_variants_r02.txt.)
