@@ -11,3 +11,6 @@ grep -E "reference arithmetic" gpurun_out/pytest_gpu_r05b.log | cut -c1-400
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_r05b.log 2>&1 || exit $?
 tail -n 1 gpurun_out/smoke_r05b.log
 bash tools/gpu_ab_cfg.sh r05b "r4|r4|" "head|-|" "r4b|r4|" "headb|-|"
+# the C3 shadow-query streams (depths 0-2, 128^2 16 spp) for the CPU stack-depth experiment
+timeout -k 10 200 python tools/dump_shadow_stream.py 128 16 > gpurun_out/dump_shadow_r05b.log 2>&1 || exit $?
+tail -1 gpurun_out/dump_shadow_r05b.log
