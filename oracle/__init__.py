@@ -14,9 +14,6 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
-# the same restatement with dot / cross / LinearSpace3 * v in the reference build's operation
-# sequences instead of the product's fused multiply-adds (yrt_oracle.c YRT_ORACLE_REF_ARITH)
-REFARITH_LIB = HERE / "liboracle_refarith.so"
 
 
 def build():
@@ -24,11 +21,10 @@ def build():
     subprocess.run(["make", "-C", str(HERE)], check=True, stdout=subprocess.DEVNULL)
 
 
-if not LIB.exists() or not REFARITH_LIB.exists():
+if not LIB.exists():
     build()
 REF_LIB = HERE / "_ref" / "libref_kat.so"  # reference-compiled KAT library (make -C oracle ref)
 _lib = C.CDLL(str(LIB))
-_reflib = C.CDLL(str(REFARITH_LIB))
 
 vp, sz, i32, PF = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_float)
 
@@ -39,17 +35,8 @@ class OracleStats(C.Structure):
 
 
 def _sig(name, res, *args):
-    for lib in (_lib, _reflib):
-        f = getattr(lib, name)
-        f.restype, f.argtypes = res, list(args)
-
-
-def _pick(arith):
-    """arith "product" (default): the vector helpers in the product's fused multiply-adds, the
-    bit-exact checker; "reference": the reference build's operation sequences."""
-    if arith not in ("product", "reference"):
-        raise ValueError(f"arith {arith!r}")
-    return _reflib if arith == "reference" else _lib
+    f = getattr(_lib, name)
+    f.restype, f.argtypes = res, list(args)
 
 
 _sig("oracle_render", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32, i32, vp, C.POINTER(OracleStats))
@@ -71,35 +58,33 @@ _sig("oracle_shuffles", None, i32, i32, i32, vp)
 _sig("oracle_libm", None, i32, i32, vp, vp, vp)
 
 
-def _err(lib=None):
-    e = (lib or _lib).oracle_last_error()
+def _err():
+    e = _lib.oracle_last_error()
     return e.decode() if e else "?"
 
 
-def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0, arith="product"):
+def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0):
     """RGB_FLOAT32 image (H, W, 3) of the frame blob; pixels outside rect stay NaN."""
     threads = threads or cpu_count()
     x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
     out = np.full((height, width, 3), np.nan, np.float32)
     st = OracleStats()
-    lib = _pick(arith)
-    rc = lib.oracle_render(blob, len(blob), width, height, gamma, x0, y0, x1, y1, threads, out.ctypes.data,
+    rc = _lib.oracle_render(blob, len(blob), width, height, gamma, x0, y0, x1, y1, threads, out.ctypes.data,
                             C.byref(st))
     if rc != 0:
-        raise RuntimeError(f"oracle_render: {_err(lib)}")
+        raise RuntimeError(f"oracle_render: {_err()}")
     return out, {n: getattr(st, n) for n, _ in st._fields_}
 
 
-def render_shard(blob: bytes, width, height, gamma, index, count, threads=0, arith="product"):
+def render_shard(blob: bytes, width, height, gamma, index, count, threads=0):
     """The tiles t % count == index of the frame (SURVEY §8(e) split); other pixels NaN."""
     threads = threads or cpu_count()
     out = np.full((height, width, 3), np.nan, np.float32)
     st = OracleStats()
-    lib = _pick(arith)
-    rc = lib.oracle_render_shard(blob, len(blob), width, height, gamma, 0, 0, width, height, index, count, threads,
+    rc = _lib.oracle_render_shard(blob, len(blob), width, height, gamma, 0, 0, width, height, index, count, threads,
                                   out.ctypes.data, C.byref(st))
     if rc != 0:
-        raise RuntimeError(f"oracle_render_shard: {_err(lib)}")
+        raise RuntimeError(f"oracle_render_shard: {_err()}")
     return out, {n: getattr(st, n) for n, _ in st._fields_}
 
 

@@ -32,25 +32,14 @@ static inline V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 static inline V3 mulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 static inline V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-#ifdef YRT_ORACLE_REF_ARITH
-/* liboracle_refarith.so: dot, cross and lmul in the reference build's operation sequence (x64
- * MSVC, SSE4.1 forced by common/sys/platform.h:100-103, no AVX2: no fused multiply-add):
+/* dot, cross and lmul in the reference build's operation sequences (x64 MSVC, SSE4.1 forced by
+ * common/sys/platform.h:100-103, no AVX2: no fused multiply-add), as the product's yrt_math.h:
  *   dot   = _mm_dp_ps(a, b, 0x7F), common/math/vector3f_sse.h:206-209: the products, then
- *           (x + y) + (z + 0) (the masked fourth lane adds +0);
+ *           (x + y) + z (dp_ps's +0 fourth lane, which only turns a -0 sum into +0, left out);
  *   cross = a0*b0 - a1*b1, vector3f_sse.h:226-233 (the non-AVX2 branch);
  *   lmul  = v.x*vx + v.y*vy + v.z*vz left to right, common/math/linearspace3.h:134. */
-static inline float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + (a.z * b.z + 0.0f); }
+static inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-#else
-/* liboracle.so: dot, cross and lmul with explicit fused multiply-adds in the order of the
- * product's yrt_math.h helpers (a documented substitution): bit-exact checking of
- * the device; the reference's sequences are the YRT_ORACLE_REF_ARITH build above. */
-static inline float dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
-static inline V3 cross(V3 a, V3 b) {
-  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
-            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
-}
-#endif
 static inline float rcp(float x) { return 1.0f / x; }
 static inline float rsqrt_(float x) { return 1.0f / sqrtf(x); }
 static inline V3 normalize(V3 a) { return muls(a, rsqrt_(dot(a, a))); }
@@ -82,15 +71,7 @@ static inline L3 l3_rows(float m00, float m01, float m02, float m10, float m11, 
   return l3(v3(m00, m10, m20), v3(m01, m11, m21), v3(m02, m12, m22));
 }
 static inline L3 l3_one(void) { return l3(v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1)); }
-#ifdef YRT_ORACLE_REF_ARITH
 static inline V3 lmul(L3 a, V3 b) { return add(add(muls(a.vx, b.x), muls(a.vy, b.y)), muls(a.vz, b.z)); }
-#else
-static inline V3 lmul(L3 a, V3 b) {
-  return v3(__builtin_fmaf(b.z, a.vz.x, __builtin_fmaf(b.y, a.vy.x, b.x * a.vx.x)),
-            __builtin_fmaf(b.z, a.vz.y, __builtin_fmaf(b.y, a.vy.y, b.x * a.vx.y)),
-            __builtin_fmaf(b.z, a.vz.z, __builtin_fmaf(b.y, a.vy.z, b.x * a.vx.z)));
-}
-#endif
 static inline L3 llmul(L3 a, L3 b) { return l3(lmul(a, b.vx), lmul(a, b.vy), lmul(a, b.vz)); }
 static inline L3 ltrans(L3 a) { return l3_rows(a.vx.x, a.vx.y, a.vx.z, a.vy.x, a.vy.y, a.vy.z, a.vz.x, a.vz.y, a.vz.z); }
 static inline L3 linv(L3 a) {

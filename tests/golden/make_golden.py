@@ -5,8 +5,7 @@
 Fixtures: embree::Random sequences (KAT 1; also pinned independently by the pure-Python
 restatement in tests/test_cpu_host.py), sample tables (KAT 2), per-tile pixel sample-set
 indices, DebugRenderer id-hash image (KAT 3), hit records of 4096 incoherent closest and
-occlusion queries on C2/C3 (KAT 4) and 64x64 RGB_FLOAT32 thumbnails of C1/C2/C4 (KAT 6; `_refarith`:
-the oracle build with the reference's dot / cross / LinearSpace3 operation sequences). The reference itself cannot run here (Embree is binary-only for Windows, SURVEY
+occlusion queries on C2/C3 (KAT 4) and 64x64 RGB_FLOAT32 thumbnails of C1/C2/C4 (KAT 6). The reference itself cannot run here (Embree is binary-only for Windows, SURVEY
 §8(c)), so these pin the restatement against regressions; parity at the Embree boundary
 is unpinned.
 """
@@ -37,9 +36,6 @@ def main():
         s = yrt.Session(args + ["-fb", "RGB_FLOAT32"], device=dev)
         img, _ = oracle.render(s.export_frame(face), 64, 64, s.info()["gamma"])
         np.save(HERE / f"thumb_{name}.npy", img)
-        # the reference build's operation sequences for dot / cross / LinearSpace3 * v
-        img, _ = oracle.render(s.export_frame(face), 64, 64, s.info()["gamma"], arith="reference")
-        np.save(HERE / f"thumb_{name}_refarith.npy", img)
         s.close()
     s = yrt.Session(c2_args(64, 1) + ["-renderer", "debug", "-fb", "RGB_FLOAT32"], device=dev)
     img, _ = oracle.render(s.export_frame(), 64, 64, 1.0)

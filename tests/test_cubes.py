@@ -173,10 +173,6 @@ def test_c4_full_size_face_band_parity(gpu_device):
     ref, st = oracle.render(s.export_frame(3), 1536, 1536, s.info()["gamma"], rect=(0, y0, 1536, y0 + 32))
     r = parity(img[y0:y0 + 32], ref[y0:y0 + 32], 0.995)
     print("C4 face 3 band", r, st["raysClosest"] + st["raysShadow"])
-    # the reference's dot / cross / LinearSpace3 sequences on 8 rows of the band
-    ref2, _ = oracle.render(s.export_frame(3), 1536, 1536, s.info()["gamma"], rect=(0, y0, 1536, y0 + 8),
-                            arith="reference")
-    print("C4 face 3 band, reference arithmetic", parity(img[y0:y0 + 8], ref2[y0:y0 + 8], 0.995, exact=False))
     s.close()
 
 
@@ -193,10 +189,6 @@ def test_c5_full_size_face_band_parity(gpu_device, cam):
                             rect=(0, y0, 1536, y0 + 16))
     r = parity(img[y0:y0 + 16], ref[y0:y0 + 16], 0.995)
     print(f"C5 face {cam} band", r, st["raysClosest"] + st["raysShadow"])
-    # the reference's dot / cross / LinearSpace3 sequences on 4 rows of the band
-    ref2, _ = oracle.render(s.export_frame(camera=s.scene_camera(cam)), 1536, 1536, s.info()["gamma"],
-                            rect=(0, y0, 1536, y0 + 4), arith="reference")
-    print(f"C5 face {cam} band, reference arithmetic", parity(img[y0:y0 + 4], ref2[y0:y0 + 4], 0.995, exact=False))
     s.close()
 
 

@@ -42,20 +42,22 @@ YRT_HD V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 YRT_HD V3 rcpv(V3 a) { return v3(1.0f / a.x, 1.0f / a.y, 1.0f / a.z); }
 YRT_HD bool operator==(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 YRT_HD bool operator!=(V3 a, V3 b) { return !(a == b); }
-// dot, cross and LinearSpace3 * v with explicit fused multiply-adds in one fixed order (one
-// correctly rounded operation on host and device; the oracle's default build uses the same
-// helpers, so every side computes the same bits): 3 instead of 5, 6 instead of 9 and 9 instead
-// of 15 operations. A documented substitution: the reference build (x64 MSVC, SSE4.1
-// forced by common/sys/platform.h:100-103, no AVX2) has no FMA — dot is _mm_dp_ps, the products
-// then (x + y) + (z + 0) (common/math/vector3f_sse.h:206-209), cross a0*b0 - a1*b1
-// (vector3f_sse.h:226-233), L * v left to right (common/math/linearspace3.h:134). The oracle's
-// -DYRT_ORACLE_REF_ARITH build follows those sequences; the product is compared with it under
-// the SURVEY §8(d) gate (tests: *_reference_arithmetic). Those sequences cost C3 1.6 % and C4
-// 1.5 % on the GPU (profiles/r05/ab_r05a.txt).
-YRT_HD float dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+// dot, cross and LinearSpace3 * v in the reference build's operation sequences (x64 MSVC, SSE4.1
+// forced by common/sys/platform.h:100-103, no AVX2, so no fused multiply-add anywhere):
+//   dot   = _mm_dp_ps(a, b, 0x7F) (common/math/vector3f_sse.h:206-209): the three products,
+//           then (x + y) + z. dp_ps adds the masked fourth lane's +0 to z's product, which
+//           changes nothing but the sign of an exactly zero sum (dp_ps never returns -0; this
+//           returns -0 when both partial sums are -0); it is left out (one VALU per dot);
+//   cross = a0*b0 - a1*b1 on shuffled operands (vector3f_sse.h:226-233, the non-AVX2 branch);
+//   L * v = v.x*vx + v.y*vy + v.z*vz, left to right (common/math/linearspace3.h:134).
+// Host setup, kernels and the oracle (oracle/yrt_oracle.c) use these same sequences. Round 4's
+// fused forms (3 / 6 / 9 instead of 5 / 9 / 15 operations, C3 +1.6 %) moved hits between
+// coplanar triangles: against this order they changed 35 % of the channels of a C5 face (the
+// Frederick stand-in's overlapping decals and walls flip with the last bit of a ray origin),
+// 1.8 % on C3 (profiles/r05/arith_sensitivity_r05.txt).
+YRT_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 YRT_HD V3 cross(V3 a, V3 b) {
-  return v3(__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
-            __builtin_fmaf(a.x, b.y, -(a.y * b.x)));
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 #if defined(__HIPCC__)
 // Correctly rounded 1/x without the general division sequence (v_div_scale x2, v_rcp, 5 FMAs,
@@ -116,11 +118,7 @@ YRT_HD L3 l3_rows(float m00, float m01, float m02, float m10, float m11, float m
   return l3(v3(m00, m10, m20), v3(m01, m11, m21), v3(m02, m12, m22));
 }
 YRT_HD L3 l3_identity() { return l3(v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1)); }
-YRT_HD V3 mul(L3 a, V3 b) {
-  return v3(__builtin_fmaf(b.z, a.vz.x, __builtin_fmaf(b.y, a.vy.x, b.x * a.vx.x)),
-            __builtin_fmaf(b.z, a.vz.y, __builtin_fmaf(b.y, a.vy.y, b.x * a.vx.y)),
-            __builtin_fmaf(b.z, a.vz.z, __builtin_fmaf(b.y, a.vy.z, b.x * a.vx.z)));
-}
+YRT_HD V3 mul(L3 a, V3 b) { return b.x * a.vx + b.y * a.vy + b.z * a.vz; }
 YRT_HD L3 mul(L3 a, L3 b) { return l3(mul(a, b.vx), mul(a, b.vy), mul(a, b.vz)); }
 YRT_HD L3 l3_rotate(V3 u_, float r) {
   V3 u = normalize(u_);

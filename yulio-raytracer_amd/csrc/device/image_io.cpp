@@ -319,7 +319,7 @@ void idct_islow(const int* in /* natural order, dequantized */, uint8_t* out, in
   for (int c = 0; c < 8; ++c) {
     const int* ip = in + c;
     if (!ip[8] && !ip[16] && !ip[24] && !ip[32] && !ip[40] && !ip[48] && !ip[56]) {
-      const int dc = ip[0] << P1;
+      const int dc = ip[0] * (1 << P1);  // a multiply: left shifts of negative values are UB (UBSan, r05)
       for (int r = 0; r < 8; ++r) ws[r * 8 + c] = dc;
       continue;
     }
@@ -329,8 +329,8 @@ void idct_islow(const int* in /* natural order, dequantized */, uint8_t* out, in
     long long tmp3 = z1 + z2 * F0765;
     z2 = ip[0];
     z3 = ip[32];
-    long long tmp0 = (z2 + z3) << CB;
-    long long tmp1 = (z2 - z3) << CB;
+    long long tmp0 = (z2 + z3) * (1ll << CB);
+    long long tmp1 = (z2 - z3) * (1ll << CB);
     const long long t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
     tmp0 = ip[56]; tmp1 = ip[40]; tmp2 = ip[24]; tmp3 = ip[8];
     z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2; long long z4 = tmp1 + tmp3;
@@ -356,8 +356,8 @@ void idct_islow(const int* in /* natural order, dequantized */, uint8_t* out, in
     long long z1 = (z2 + z3) * F0541;
     long long tmp2 = z1 + z3 * (-F1847);
     long long tmp3 = z1 + z2 * F0765;
-    long long tmp0 = ((long long)w[0] + w[4]) << CB;
-    long long tmp1 = ((long long)w[0] - w[4]) << CB;
+    long long tmp0 = ((long long)w[0] + w[4]) * (1ll << CB);
+    long long tmp1 = ((long long)w[0] - w[4]) * (1ll << CB);
     const long long t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
     tmp0 = w[7]; tmp1 = w[5]; tmp2 = w[3]; tmp3 = w[1];
     z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2; long long z4 = tmp1 + tmp3;

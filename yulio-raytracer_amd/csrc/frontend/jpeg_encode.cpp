@@ -114,8 +114,8 @@ void fdct_islow(int32_t d[64]) {
     int64_t t0 = p[0] + p[7], t7 = p[0] - p[7], t1 = p[1] + p[6], t6 = p[1] - p[6];
     int64_t t2 = p[2] + p[5], t5 = p[2] - p[5], t3 = p[3] + p[4], t4 = p[3] - p[4];
     int64_t t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
-    p[0] = (int32_t)((t10 + t11) << P1);
-    p[4] = (int32_t)((t10 - t11) << P1);
+    p[0] = (int32_t)((t10 + t11) * (1 << P1));  // multiplies: left shifts of negative values are UB
+    p[4] = (int32_t)((t10 - t11) * (1 << P1));
     int64_t z1 = (t12 + t13) * F0541;
     p[2] = descale(z1 + t13 * F0765, CB - P1);
     p[6] = descale(z1 + t12 * (-F1847), CB - P1);
