@@ -194,6 +194,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s scenes|images|fuzz|hub ...\n", argv[0]);
     return 2;
   }
+  setvbuf(stdout, nullptr, _IOLBF, 0);  // progress lines reach the log as they happen
   const std::string mode = argv[1];
   if (mode == "hub") {
     const int bad = hub_rounds(argc > 2 ? atoi(argv[2]) : 4);

@@ -127,3 +127,25 @@ def test_stoprt_cancels_a_running_render(tmp_path):
     assert st.state == 3  # Stopped
     assert not (tmp_path / "cornell_box_cubemap.jpg").exists()
     assert not yrt.WaitRT()  # nothing left to wait for
+
+
+@pytest.mark.parametrize("mangle", [
+    ("<!-- light -->", "<!-\r light -->"),          # a broken comment opener (fuzz finding, r05)
+    ('<float name="eta">', '<float name="eta>'),    # an attribute value without its closing quote
+    ('<float name="eta">', '<float name=eta>'),     # an unquoted attribute value
+    ("</scene>", "</scene"),                        # an end tag without '>'
+    ("<Group>", "<>"),                              # an empty element name
+], ids=["comment", "quote", "unquoted", "endtag", "noname"])
+def test_malformed_xml_fails_cleanly(host_device, tmp_path, mangle):
+    """The XML scene reader refuses malformed text with an error instead of looping: a mangled
+    comment opener once wrapped its scan index past npos back to 0 and parsed forever
+    (tools/run_sanitizers.sh mutation fuzz, profiles/r05/sanitizers_r05.txt)."""
+    import time
+    src = (SCENES / "cornell_box_spheres.xml").read_text()
+    assert mangle[0] in src
+    f = tmp_path / "mangled.xml"
+    f.write_text(src.replace(mangle[0], mangle[1], 1))
+    t = time.perf_counter()
+    with pytest.raises(RuntimeError):
+        yrt.Session(["-i", str(f), "-size", "16", "16"], device=host_device)
+    assert time.perf_counter() - t < 10

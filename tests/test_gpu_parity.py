@@ -517,4 +517,12 @@ def test_framebuffer_read_back_at_map(gpu_device):
     assert np.array_equal(d.framebuffer_array(fb, 64, 64, "RGB_FLOAT32"), ref[5])
     assert np.array_equal(d.framebuffer_array(fc, 64, 64, "RGB_FLOAT32"), ref[0])
     assert np.array_equal(d.framebuffer_array(fa, 64, 64, "RGB_FLOAT32"), ref[9])  # a second map: same pixels
+    # eight framebuffers rendered before any map: past three live frame blocks the block about to
+    # be reused is read back to its framebuffers' host pixels (GpuCtx::kMaxFrameBlocks)
+    fbs = [d.rtNewFrameBuffer("RGB_FLOAT32", 64, 64) for _ in range(8)]
+    faces = [0, 5, 9, 0, 5, 9, 0, 5]
+    for f, cam in zip(fbs, faces):
+        d.rtRenderFrame(R, s.camera(cam), S, T, f, 0)
+    for f, cam in zip(fbs, faces):
+        assert np.array_equal(d.framebuffer_array(f, 64, 64, "RGB_FLOAT32"), ref[cam])
     s.close()

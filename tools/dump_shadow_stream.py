@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Dumps the C3 frame's complete shadow-query streams of depths 0-2 (batch 0, queue order) plus the
+"""Dumps the C3 frame's complete shadow- and closest-query streams of depths 0-2 (batch 0, queue order) plus the
 uploaded BVH to gpurun_out/shadow_c3.npz, for CPU-side any-hit experiments
 (tools/occluder_cache_exp.c). usage: python tools/dump_shadow_stream.py [size] [spp]"""
 import sys
@@ -24,6 +24,8 @@ out = {}
 for depth in range(3):
     org, dr, tot = dev.captured_rays(1, depth)
     out[f"s{depth}_org"], out[f"s{depth}_dir"] = org, dr
+    org, dr, tot = dev.captured_rays(0, depth)  # the closest-hit queries entering this depth
+    out[f"c{depth}_org"], out[f"c{depth}_dir"] = org, dr
 nodes, tris = dev.export_bvh(S)
 out["nodes"], out["tris"] = nodes, tris
 Path(ROOT / "gpurun_out").mkdir(exist_ok=True)

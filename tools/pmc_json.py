@@ -26,7 +26,7 @@ from collections import defaultdict
 from pathlib import Path
 
 SIMDS, XCDS = 256 * 4, 8
-KERNELS = {"k_trace<false>": "k_trace<false", "k_trace<true>": "k_trace<true", "k_shade": "k_shade", "k_raygen": "k_raygen",
+KERNELS = {"k_trace<false>": "k_trace<false", "k_trace<true>": "k_trace<true", "k_occluded": "k_occluded", "k_shade": "k_shade", "k_raygen": "k_raygen",
            "k_shadow_resolve": "k_shadow_resolve", "k_resolve_pixels": "k_resolve_pixels",
            "k_valu_calib": "k_valu_calib"}
 

@@ -88,6 +88,10 @@ struct GpuCtx {
     long long zeroKey[5] = {-1, -1, -1, -1, -1};
   };
   std::shared_ptr<FrameBlock> blk = std::make_shared<FrameBlock>(), spareBlk;
+  // every block allocated after the first two (weak: a block lives while a framebuffer's
+  // unread frame or blk / spareBlk holds it); at most kMaxFrameBlocks stay alive
+  static constexpr int kMaxFrameBlocks = 3;
+  std::vector<std::weak_ptr<FrameBlock>> extraBlocks;
   float* fbFloat() const { return blk->fbFloat.as<float>(); }
   uint8_t* fbRGB8() const { return blk->fbRGB8.as<uint8_t>(); }
   std::vector<int> hDirect;        // the frame's direct-light list (uploaded to dDirect)
@@ -201,6 +205,8 @@ static int shard_tiles(int numTiles, int index, int count) {
   return numTiles > index ? (numTiles - index + count - 1) / count : 0;
 }
 
+void fb_read_back(FrameBufferObj& F, int id);
+
 class Device {
  public:
   std::recursive_mutex mu;
@@ -300,7 +306,19 @@ class Device {
   // the render's output is this shard alone (no gather fills the other shards' tiles): those
   // pixels must read as zeros, so per-shard images compose by sum
   bool shardZero = true;
-  void gather_process(const SlabLayout& base, int numTiles, bool localOk);
+  // renderSeconds: this rank's render time of the call; the status exchange waits for the
+  // slowest rank's render, so its deadline is gatherTimeout + kStatusRenderFactor x that time
+  // (a peer may take ten times as long before the gather gives up; the slab transfers keep
+  // gatherTimeout)
+  static constexpr double kStatusRenderFactor = 10.0;
+  void gather_process(const SlabLayout& base, int numTiles, bool localOk, double renderSeconds);
+  // copies every unread frame held in block b into its framebuffer's host pixels
+  void read_back_block(const void* b) {
+    for (HandleRef* h : handles)
+      if (auto* F = dynamic_cast<FrameBufferObj*>(h->obj.get()))
+        for (int id = 0; id < (int)F->pending.size(); ++id)
+          if (F->pending[id].keep.get() == b) fb_read_back(*F, id);
+  }
   // a process gather is armed: every render of this device joins the ranks' status exchange
   bool proc_gather_armed() const {
     return proc && shardCount > 1 && shardIndex == commRank && shardCount == commWorld;
@@ -396,11 +414,26 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     memset(&stats, 0, sizeof(stats));
     if (!accumulate) R.iteration = 0;
     {
-      // frames of an earlier job not yet read back: this job renders into another block
+      // frames of an earlier job not yet read back: this job renders into another block. With
+      // blk and spareBlk both holding unread frames a new block is allocated, up to
+      // kMaxFrameBlocks alive; past that the block about to be reused is read back into its
+      // framebuffers' host pixels first (rtMapFrameBuffer then finds them there), so frames
+      // nobody maps cannot pin HBM without bound
       GpuCtx& g0 = *ctx[0];
       if (g0.blk.use_count() > 1) {
         std::swap(g0.blk, g0.spareBlk);
-        if (!g0.blk || g0.blk.use_count() > 1) g0.blk = std::make_shared<GpuCtx::FrameBlock>();
+        if (!g0.blk || g0.blk.use_count() > 1) {
+          auto& xb = g0.extraBlocks;
+          xb.erase(std::remove_if(xb.begin(), xb.end(), [](const std::weak_ptr<GpuCtx::FrameBlock>& w) {
+                     return w.expired();
+                   }), xb.end());
+          if (g0.blk && 2 + (int)xb.size() >= GpuCtx::kMaxFrameBlocks) {
+            read_back_block(g0.blk.get());
+          } else {
+            g0.blk = std::make_shared<GpuCtx::FrameBlock>();
+            xb.push_back(g0.blk);
+          }
+        }
       }
     }
     std::vector<GpuScene*> scenes(nr);
@@ -435,7 +468,8 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     localErr = e.what();
   }
   if (procGather) {
-    gather_process(base, numTiles, localErr.empty());
+    gather_process(base, numTiles, localErr.empty(),
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     gatherPath = proc->kind()[0] == 'r' ? YRT_GATHER_RCCL_PROCESS : YRT_GATHER_HUB;
   }
   if (!localErr.empty()) throw std::runtime_error(localErr);
@@ -1010,12 +1044,14 @@ int Device::gather_local(const SlabLayout& base, int numTiles) {
 // yrtSetShardHub): the ranks first exchange their render status (the min of every rank's
 // flag, so a rank whose render failed makes every rank fail instead of leaving rank 0 waiting
 // for its slab), then every rank packs its tiles and rank 0 receives each peer's slab and
-// unpacks it into its frames. Every wait is bounded by gatherTimeout.
-void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk) {
+// unpacks it into its frames. Every wait is bounded: the status exchange by gatherTimeout plus
+// kStatusRenderFactor times this rank's render time, the transfers by gatherTimeout.
+void Device::gather_process(const SlabLayout& base, int numTiles, bool localOk, double renderSeconds) {
   GpuCtx& g0 = *ctx[0];
   HIP_CHECK(hipSetDevice(g0.hipDevice));
   const int P = shardCount;
-  const int flag = proc->exchange_status(localOk ? 1 : 0, g0.hipDevice, g0.stream, gatherTimeout);
+  const int flag = proc->exchange_status(localOk ? 1 : 0, g0.hipDevice, g0.stream,
+                                         gatherTimeout + kStatusRenderFactor * std::max(0.0, renderSeconds));
   if (!flag) {
     if (localOk) throw std::runtime_error("rtRenderFrame: a peer rank's render failed (no frame gathered)");
     return;  // the caller rethrows this rank's own error

@@ -124,7 +124,12 @@ struct XmlReader {
       }
     }
   }
-  XMLp node() {
+  // Every scan is bounded by the end of the text and every malformed construct throws: a
+  // truncated or mangled file (a broken comment opener, an attribute without its quote, an
+  // end tag without '>') used to wrap an index past std::string::npos back to the start and
+  // loop forever (found by the sanitizer driver's mutation fuzz, tools/run_sanitizers.sh).
+  XMLp node(int depth = 0) {
+    if (depth > 512) throw std::runtime_error(where() + ": elements nested too deeply");
     skipMisc();
     if (i >= s.size() || s[i] != '<') throw std::runtime_error(where() + ": '<' expected");
     auto x = std::make_shared<XML>();
@@ -133,22 +138,27 @@ struct XmlReader {
     size_t b = i;
     while (i < s.size() && !isspace((unsigned char)s[i]) && s[i] != '>' && s[i] != '/') i++;
     x->name = s.substr(b, i - b);
+    if (x->name.empty()) throw std::runtime_error(x->loc + ": element name expected");
     for (;;) {
       ws();
       if (i >= s.size()) throw std::runtime_error(where() + ": unterminated tag");
       if (s[i] == '/') {
-        i += 2;  // "/>"
+        if (s.compare(i, 2, "/>") != 0) throw std::runtime_error(where() + ": '/>' expected");
+        i += 2;
         return x;
       }
       if (s[i] == '>') { i++; break; }
       b = i;
-      while (i < s.size() && s[i] != '=' && !isspace((unsigned char)s[i])) i++;
+      while (i < s.size() && s[i] != '=' && s[i] != '>' && s[i] != '/' && !isspace((unsigned char)s[i])) i++;
       std::string key = s.substr(b, i - b);
       ws();
+      if (key.empty() || i >= s.size() || s[i] != '=') throw std::runtime_error(where() + ": malformed attribute");
       i++;  // '='
       ws();
+      if (i >= s.size() || (s[i] != '"' && s[i] != '\'')) throw std::runtime_error(where() + ": quoted value expected");
       const char q = s[i++];
-      size_t e = s.find(q, i);
+      const size_t e = s.find(q, i);
+      if (e == std::string::npos) throw std::runtime_error(where() + ": unterminated attribute value");
       x->parms[key] = s.substr(i, e - i);
       i = e + 1;
     }
@@ -157,18 +167,19 @@ struct XmlReader {
       size_t b2 = i;
       while (i < s.size() && s[i] != '<') i++;
       tokens(s.substr(b2, i - b2), x->body);
+      if (i >= s.size()) throw std::runtime_error(where() + ": unexpected end of file");
       if (s.compare(i, 4, "<!--") == 0) {
         size_t e = s.find("-->", i);
         i = e == std::string::npos ? s.size() : e + 3;
         continue;
       }
       if (s.compare(i, 2, "</") == 0) {
-        size_t e = s.find('>', i);
+        const size_t e = s.find('>', i);
+        if (e == std::string::npos) throw std::runtime_error(where() + ": unterminated end tag");
         i = e + 1;
         return x;
       }
-      if (i >= s.size()) throw std::runtime_error(where() + ": unexpected end of file");
-      x->children.push_back(node());
+      x->children.push_back(node(depth + 1));
     }
   }
 };

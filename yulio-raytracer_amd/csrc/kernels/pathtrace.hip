@@ -2081,8 +2081,8 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, const float* time) {
   const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   const ShadowFuse sf = fuse ? *fuse : ShadowFuse{};
-  // static scenes: two rays per lane (k_occluded); YRT_ANY2=0 keeps one (A/B switch)
-  static const bool two = !getenv("YRT_ANY2") || atoi(getenv("YRT_ANY2")) != 0;
+  // YRT_ANY2=1: two rays per lane (k_occluded, static scenes) — measured slower, off (A/B switch)
+  static const bool two = getenv("YRT_ANY2") && atoi(getenv("YRT_ANY2")) != 0;
   if (!time && two) {
     hipLaunchKernelGGL(k_occluded, grid, dim3(64), 0, s, sv, org, dir, counts, numSegs, segCap, occluded,
                        sv.traceSpill, sf);
