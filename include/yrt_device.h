@@ -225,8 +225,9 @@ typedef struct YRTShardHub_* YRTShardHub;
 YRT_API YRTShardHub yrtNewShardHub(int world);
 YRT_API void yrtDeleteShardHub(YRTShardHub hub);
 YRT_API int yrtSetShardHub(YRTDevice dev, YRTShardHub hub, int rank);
-/* Bound, in seconds, of every wait of a gather (status exchange, slab send/recv); default
- * YRT_GATHER_TIMEOUT_S or 300. The status exchange also waits for the slowest rank's render. */
+/* Bound, in seconds, of the waits of a gather; default YRT_GATHER_TIMEOUT_S or 300. The slab
+ * send/recv wait at most this long; the status exchange, which also waits for the slowest rank's
+ * render, this plus ten times the calling rank's render time of the frame. */
 YRT_API int yrtSetGatherTimeout(YRTDevice dev, double seconds);
 /* Host-memory forms of the hub's two phases (CPU tests of its deadlines and size checks):
  * yrtShardHubStatus returns the min of the ranks' flags (or -1), yrtShardHubSlab sends `bytes`

@@ -149,3 +149,19 @@ def test_malformed_xml_fails_cleanly(host_device, tmp_path, mangle):
     with pytest.raises(RuntimeError):
         yrt.Session(["-i", str(f), "-size", "16", "16"], device=host_device)
     assert time.perf_counter() - t < 10
+
+
+def test_obj_short_faces_and_mixed_normals(host_device, tmp_path):
+    """OBJ faces of fewer than three vertices yield no triangle (the fan read face[1] of a
+    one-vertex face: a heap overread under ASan, tools/run_sanitizers.sh mutation fuzz), and a
+    group mixing vertices with and without normals is refused instead of handing the mesh a
+    normal array shorter than its positions."""
+    f = tmp_path / "short.obj"
+    f.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1\nf 1 2\nf 1 2 3\n")
+    s = yrt.Session(["-i", str(f), "-size", "16", "16"], device=host_device)
+    assert host_device.scene_info(s.info()["scene"])["numTriangles"] == 1
+    s.close()
+    g = tmp_path / "mixed.obj"
+    g.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nv 1 1 0\nvn 0 0 1\nf 1//1 2//1 3//1\nf 2 4 3\n")
+    with pytest.raises(RuntimeError, match="normals"):
+        yrt.Session(["-i", str(g), "-size", "16", "16"], device=host_device)

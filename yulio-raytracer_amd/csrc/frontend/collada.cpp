@@ -128,10 +128,10 @@ const char* atoreal(const char* c, float& out) {
 long strtol10(const char* in, const char** out) {
   const bool inv = (*in == '-');
   if (inv || *in == '+') ++in;
-  long v = 0;
-  while (is_digit(*in)) v = v * 10 + (*in++ - '0');
+  unsigned long v = 0;  // unsigned: an over-long digit run wraps instead of overflowing (UB)
+  while (is_digit(*in)) v = v * 10 + (unsigned long)(*in++ - '0');
   *out = in;
-  return inv ? -v : v;
+  return inv ? -(long)v : (long)v;
 }
 
 // ---------------------------------------------------------------- XML DOM
@@ -649,8 +649,9 @@ struct Parser {
         const size_t count = cnt ? (size_t)atol(cnt) : 0;
         std::vector<float>& v = data[id ? id : ""];
         v.clear();
-        v.reserve(count);
         const char* t = d.text(k);
+        // a value takes at least two characters of text: a corrupt count cannot reserve more
+        v.reserve(std::min(count, strlen(t) / 2 + 1));
         for (size_t a = 0; a < count; ++a) {
           skip_space(t);
           if (!*t) throw std::runtime_error("Collada: Expected more values while reading float_array contents.");
@@ -775,7 +776,9 @@ struct Parser {
           for (size_t a = 0; a < numPrims; ++a) {
             skip_space(t);
             if (!*t) throw std::runtime_error("Collada: Expected more values while reading <vcount> contents.");
+            const char* t0 = t;
             long v = strtol10(t, &t);
+            if (t == t0) throw std::runtime_error("Collada: unexpected character in <vcount> element");
             vcount.push_back((size_t)v);
           }
         }
@@ -803,7 +806,12 @@ struct Parser {
       const char* t = d.text(p);
       skip_space(t);
       while (*t) {
+        const char* t0 = t;
         const long v = strtol10(t, &t);
+        // a character that is neither a number nor a space would leave t where it is (Assimp's
+        // loop, ColladaParser.cpp:2306, spins there pushing zeros until memory runs out):
+        // refuse the file instead (mutation fuzz finding, tools/run_sanitizers.sh)
+        if (t == t0) throw std::runtime_error("Collada: unexpected character in <p> element");
         idx.push_back((size_t)std::max(0l, v));
         skip_space(t);
       }

@@ -673,6 +673,9 @@ struct OBJLoader {
       return vertexMap[i] = (int)(positions.size() / 3) - 1;
     };
     for (auto& face : curGroup) {
+      // a face of fewer than three vertices yields no triangle (the reference's fan reads
+      // face[1] regardless: a heap overread on "f 1", found by the mutation fuzz)
+      if (face.size() < 3) continue;
       OVertex i0 = face[0], i1{-1, -1, -1}, i2 = face[1];
       for (size_t k = 2; k < face.size(); k++) {
         i1 = i2;
@@ -682,6 +685,12 @@ struct OBJLoader {
       }
     }
     curGroup.clear();
+    // vertices with and without normals (or texture coordinates) in one group would give
+    // arrays shorter than the positions, which the mesh would index past their end
+    if ((!normals.empty() && normals.size() != positions.size()) ||
+        (!texcoords.empty() && texcoords.size() / 2 != positions.size() / 3))
+      throw std::runtime_error("OBJ: a face group mixes vertices with and without normals or texture coordinates");
+    if (triangles.empty()) return;
     YRTHandle dp = checkH(dev, yrtNewData(dev, "immutable", positions.size() * 4, positions.data()), "rtNewData");
     YRTHandle dt = checkH(dev, yrtNewData(dev, "immutable", triangles.size() * 4, triangles.data()), "rtNewData");
     YRTHandle mesh = checkH(dev, yrtNewShape(dev, "trianglemesh"), "rtNewShape");

@@ -48,12 +48,7 @@ struct SceneView {
 #ifndef YRT_TRACE_GRID
 #define YRT_TRACE_GRID 16384
 #endif
-// spilled stack entries per lane: the one-ray kernels' (YRT_STACK_DEPTH - ring) or two ray slots
-// of k_occluded's (one 64-lane wave per block, YRT_TRACE_GRID blocks at most)
-#define YRT_SPILL_PER_LANE                                                                     \
-  ((YRT_STACK_DEPTH - YRT_LDS_STACK_MIN) > 2 * (YRT_STACK_DEPTH - YRT_ANY2_LDS) ? (YRT_STACK_DEPTH - YRT_LDS_STACK_MIN) \
-                                                                              : 2 * (YRT_STACK_DEPTH - YRT_ANY2_LDS))
-#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * (YRT_TRACE_BLOCK > 64 ? YRT_TRACE_BLOCK : 64) * YRT_SPILL_PER_LANE)
+#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * YRT_TRACE_BLOCK * (YRT_STACK_DEPTH - YRT_LDS_STACK_MIN))
 
 struct FrameView {
   const GpuRenderParams* rp;   // device copy

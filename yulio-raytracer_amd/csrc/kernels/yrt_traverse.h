@@ -34,10 +34,6 @@ static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be
 #endif
 static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
 #define YRT_LDS_STACK_MIN (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
-#ifndef YRT_ANY2_LDS
-#define YRT_ANY2_LDS 16  // LDS ring entries per ray slot of the two-ray any-hit kernel (k_occluded)
-#endif
-static_assert((YRT_ANY2_LDS & (YRT_ANY2_LDS - 1)) == 0, "YRT_ANY2_LDS must be a power of two");
 #ifndef YRT_TRACE_BLOCK
 // one wave per block (8 KB of LDS stack): +1.0 % on C3 over 128-lane blocks once the trace code
 // was scheduled for a 6-wave target (profiles/r01/variants_r01.txt)
