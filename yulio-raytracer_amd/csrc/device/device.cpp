@@ -1807,6 +1807,13 @@ int yrtSetKernelTiming(YRTDevice dev, int enable) {
   return 0;
   DEV_END(-1)
 }
+int yrtSetLanes(YRTDevice dev, int lanes) {
+  DEV_GUARD(dev, -1)
+  if (lanes < 1 || lanes > GpuCtx::kMaxLanes) throw std::runtime_error("yrtSetLanes: 1..4 lanes");
+  for (auto& c : dev->d->ctx) c->numLanes = lanes;
+  return 0;
+  DEV_END(-1)
+}
 int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out) {
   DEV_GUARD(dev, -1)
   auto S = dev->d->get<SceneObj>(scene, "scene");

@@ -303,6 +303,10 @@ class Device:
     def set_kernel_timing(self, on=True):
         self._rc(N.dev.yrtSetKernelTiming(self.h, int(on)), "set_kernel_timing")
 
+    def set_lanes(self, lanes):
+        """Wavefront lanes (overlapping HIP streams), 1..4; with 1 no two kernels overlap."""
+        self._rc(N.dev.yrtSetLanes(self.h, int(lanes)), "set_lanes")
+
     def scene_info(self, scene) -> dict:
         s = SceneInfo()
         self._rc(N.dev.yrtGetSceneInfo(self.h, scene, C.byref(s)), "scene_info")

@@ -138,6 +138,7 @@ _sig(dev, "yrtOccluded", i32, vp, vp, vp, vp, C.c_uint32, vp, vp)
 _sig(dev, "yrtTriangleIds", i32, vp, vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32))
 _sig(dev, "yrtGetRenderStats", i32, vp, C.POINTER(RenderStats))
 _sig(dev, "yrtSetKernelTiming", i32, vp, i32)
+_sig(dev, "yrtSetLanes", i32, vp, i32)
 _sig(dev, "yrtGetSceneInfo", i32, vp, vp, C.POINTER(SceneInfo))
 _sig(dev, "yrtExportBVH", i32, vp, vp, vp, sz, vp, sz)
 _sig(dev, "yrtExportFrame", C.c_int64, vp, vp, vp, vp, vp, sz)
