@@ -34,8 +34,9 @@ SCENES=$(ls scenes/*.ecs scenes/*.xml scenes/samples/*.ecs scenes/samples/*.xml 
   scenes/_generated/*.ecs scenes/_generated/*.dae "$GEN"/*.dae)
 IMAGES=$(ls scenes/*.png scenes/*.ppm scenes/Sponza/*.JPG scenes/frederick/*.jpg scenes/frederick/*.jpeg scenes/frederick/*.png)
 FUZZ="$GEN/room.dae scenes/cornell_box.obj scenes/cornell_box.mtl scenes/cornell_box.ecs scenes/cornell_box_spheres.xml \
-  scenes/test_stereo.xml scenes/logo.png scenes/frederick/Kitchen_Sink.jpg scenes/frederick/Metal_Aluminum_Anodized.jpg \
-  scenes/lines.ppm"
+  scenes/test_stereo.xml scenes/test_stereo_view.ecs scenes/materials_lights.ecs scenes/samples/sphere_motion.xml \
+  scenes/logo.png scenes/frederick/material_77.png scenes/frederick/Kitchen_Sink.jpg \
+  scenes/frederick/Metal_Aluminum_Anodized.jpg scenes/frederick/Brick_Antique_01.jpg scenes/lines.ppm"
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=0:detect_stack_use_after_return=1
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
 export TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1

@@ -87,6 +87,11 @@ static bool load_ppm(const std::string& file, ImageObj& out) {
   }
   int width, height, maxColor;
   if (fscanf(f, "%i %i %i", &width, &height, &maxColor) != 3) { fclose(f); return false; }
+  // the pixel array is allocated from these (a corrupt header must not ask for terabytes)
+  if (width < 1 || height < 1 || (int64_t)width * height > (int64_t(1) << 28) || maxColor < 1 || maxColor > 65535) {
+    fclose(f);
+    return false;
+  }
   const float rcpMaxColor = 1.0f / float(maxColor);
   fgetc(f);
   out.width = width;
@@ -142,6 +147,7 @@ bool decode_png(const std::vector<uint8_t>& f, int& w, int& h, int& channels, st
     if (pos + 12 + len > f.size()) { err = "truncated chunk"; return false; }
     const uint8_t* d = &f[pos + 8];
     if (!memcmp(t, "IHDR", 4)) {
+      if (len < 13) { err = "truncated IHDR"; return false; }
       w = (int)be32(d);
       h = (int)be32(d + 4);
       depth = d[8];
@@ -155,6 +161,8 @@ bool decode_png(const std::vector<uint8_t>& f, int& w, int& h, int& channels, st
     pos += 12 + len;
   }
   if (depth != 8 || interlace != 0) { err = "only 8-bit non-interlaced PNG"; return false; }
+  // the inflate buffer is allocated from these: refuse what no texture needs (256 Mpx)
+  if (w < 1 || h < 1 || (int64_t)w * h > (int64_t(1) << 28)) { err = "bad PNG dimensions"; return false; }
   if (ctype == 2) channels = 3;
   else if (ctype == 6) channels = 4;
   else if (ctype == 4) channels = 2;
@@ -170,10 +178,10 @@ bool decode_png(const std::vector<uint8_t>& f, int& w, int& h, int& channels, st
   px.assign(stride * h, 0);
   const int bpp = channels;
   for (int y = 0; y < h; ++y) {
-    const uint8_t ft = raw[y * (stride + 1)];
-    const uint8_t* s = &raw[y * (stride + 1) + 1];
-    uint8_t* o = &px[y * stride];
-    const uint8_t* up = y ? &px[(y - 1) * stride] : nullptr;
+    const uint8_t ft = raw[(size_t)y * (stride + 1)];
+    const uint8_t* s = &raw[(size_t)y * (stride + 1) + 1];
+    uint8_t* o = &px[(size_t)y * stride];
+    const uint8_t* up = y ? &px[(size_t)(y - 1) * stride] : nullptr;
     for (size_t i = 0; i < stride; ++i) {
       const int a = i >= (size_t)bpp ? o[i - bpp] : 0;
       const int b = up ? up[i] : 0;
@@ -243,6 +251,7 @@ struct Huff {
   uint8_t bits[17] = {0};
   uint8_t vals[256] = {0};
   int mincode[17], maxcode[18], valptr[17];
+  Huff() { build(); }  // an absent table decodes nothing instead of reading uninitialized bounds
   void build() {
     int code = 0, k = 0;
     for (int l = 1; l <= 16; ++l) {
@@ -289,9 +298,11 @@ struct BitReader {
     return (acc >> n) & 1;
   }
   int bits(int k) {
-    int v = 0;
-    for (int i = 0; i < k; ++i) v = (v << 1) | getbit();
-    return v;
+    // a corrupt table can ask for more than the 16 bits a baseline JPEG ever reads: take at
+    // most 16 (unsigned, so no shift overflows; mutation fuzz finding)
+    unsigned v = 0;
+    for (int i = 0; i < k && i < 16; ++i) v = (v << 1) | (unsigned)getbit();
+    return (int)v;
   }
   void reset() { n = 0; marker = false; }
 };
@@ -378,7 +389,7 @@ void idct_islow(const int* in /* natural order, dequantized */, uint8_t* out, in
 
 bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uint8_t>& rgb, std::string& err) {
   if (f.size() < 4 || f[0] != 0xFF || f[1] != 0xD8) { err = "not a JPEG"; return false; }
-  uint16_t q[4][64];
+  uint16_t q[4][64] = {};
   Huff dc[4], ac[4];
   std::vector<Comp> comps;
   int restart = 0;
@@ -392,13 +403,18 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
     if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01 || m == 0xFF) continue;
     if (m == 0xD9) break;
     const size_t len = (size_t)f[pos] << 8 | f[pos + 1];
+    // every marker segment must lie inside the file, and every table inside its segment
+    // (the mutation fuzz of tools/run_sanitizers.sh found reads past both ends)
+    if (len < 2 || pos + len > f.size()) { err = "truncated JPEG segment"; return false; }
     const uint8_t* d = &f[pos + 2];
     const size_t seg = pos + len;
+    const size_t dl = len - 2;  // payload bytes of the segment
     if (m == 0xDB) {
       size_t i = 0;
-      while (i + 1 < len - 2) {
+      while (i + 1 < dl) {
         const int pq = d[i] >> 4, tq = d[i] & 15;
         i++;
+        if (i + (pq ? 128 : 64) > dl) { err = "truncated quantization table"; return false; }
         for (int k = 0; k < 64; ++k) {
           const int v = pq ? (d[i] << 8 | d[i + 1]) : d[i];
           i += pq ? 2 : 1;
@@ -407,27 +423,38 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
       }
     } else if (m == 0xC4) {
       size_t i = 0;
-      while (i < len - 2) {
+      while (i < dl) {
+        if (i + 17 > dl) { err = "truncated Huffman table"; return false; }
         const int tc = d[i] >> 4, th = d[i] & 3;
         Huff& hh = tc ? ac[th] : dc[th];
         int total = 0;
         for (int l = 1; l <= 16; ++l) { hh.bits[l] = d[i + l]; total += d[i + l]; }
+        if (total > 256 || i + 17 + (size_t)total > dl) { err = "bad Huffman table"; return false; }
         for (int k = 0; k < total; ++k) hh.vals[k] = d[i + 17 + k];
         hh.present = true;
         hh.build();
         i += 17 + total;
       }
     } else if (m == 0xC0 || m == 0xC1) {
+      if (frame) { err = "second frame header"; return false; }
+      if (dl < 6) { err = "truncated frame header"; return false; }
       if (d[0] != 8) { err = "12-bit JPEG"; return false; }
       Hh = d[1] << 8 | d[2];
       W = d[3] << 8 | d[4];
       const int nc = d[5];
+      if (nc < 1 || nc > 4 || dl < 6 + 3 * (size_t)nc) { err = "bad frame header"; return false; }
+      // decoded planes are allocated from these: refuse what no texture needs (256 Mpx)
+      if (W < 1 || Hh < 1 || (int64_t)W * Hh > (int64_t(1) << 28)) { err = "bad JPEG dimensions"; return false; }
       comps.resize(nc);
       for (int c = 0; c < nc; ++c) {
         comps[c].id = d[6 + 3 * c];
         comps[c].H = d[7 + 3 * c] >> 4;
         comps[c].V = d[7 + 3 * c] & 15;
         comps[c].tq = d[8 + 3 * c];
+        if (comps[c].H < 1 || comps[c].H > 4 || comps[c].V < 1 || comps[c].V > 4) {
+          err = "bad sampling factors";
+          return false;
+        }
         Hmax = std::max(Hmax, comps[c].H);
         Vmax = std::max(Vmax, comps[c].V);
       }
@@ -445,10 +472,13 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
       err = "progressive/lossless/arithmetic JPEG not supported";
       return false;
     } else if (m == 0xDD) {
+      if (dl < 2) { err = "truncated restart interval"; return false; }
       restart = d[0] << 8 | d[1];
     } else if (m == 0xDA) {
       if (!frame) { err = "SOS before SOF"; return false; }
+      if (dl < 1) { err = "truncated scan header"; return false; }
       const int ns = d[0];
+      if (ns < 1 || dl < 1 + 2 * (size_t)ns) { err = "bad scan header"; return false; }
       std::vector<Comp*> sc;
       for (int i = 0; i < ns; ++i) {
         for (auto& c : comps)
@@ -458,16 +488,17 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
             sc.push_back(&c);
           }
       }
+      if (sc.empty()) { err = "scan without a frame component"; return false; }
       BitReader br;
-      br.p = &f[seg];
+      br.p = f.data() + seg;
       br.end = f.data() + f.size();
       for (auto* c : sc) c->pred = 0;
       int coef[64], deq[64];
       auto block = [&](Comp& c, int bx, int by) {
         memset(coef, 0, sizeof(coef));
-        const int t = decode_huff(br, dc[c.td & 3]);
+        const int t = std::min(decode_huff(br, dc[c.td & 3]), 16);  // categories beyond 16: corrupt data
         const int diff = t ? extend(br.bits(t), t) : 0;
-        c.pred += diff;
+        c.pred = (int)((unsigned)c.pred + (unsigned)diff);  // corrupt data: wrap, not overflow
         coef[0] = c.pred;
         for (int k = 1; k < 64;) {
           const int rs = decode_huff(br, ac[c.ta & 3]);
@@ -481,7 +512,11 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
           coef[kZigzag[k]] = extend(br.bits(s), s);
           k++;
         }
-        for (int k = 0; k < 64; ++k) deq[k] = coef[k] * (int)q[c.tq & 3][k];
+        for (int k = 0; k < 64; ++k) {
+          // valid data stays far inside int; corrupt coefficients are clamped, not overflowed
+          const long long v = (long long)coef[k] * q[c.tq & 3][k];
+          deq[k] = (int)std::max(-(1ll << 24), std::min(v, 1ll << 24));
+        }
         const int stride = c.bw * 8;
         idct_islow(deq, &c.plane[(size_t)by * 8 * stride + bx * 8], stride);
       };
@@ -523,6 +558,8 @@ bool decode_jpeg(const std::vector<uint8_t>& f, int& W, int& Hh, std::vector<uin
     pos = seg;
   }
   if (!frame) { err = "no frame"; return false; }
+  for (const Comp& c : comps)
+    if (Hmax % c.H || Vmax % c.V) { err = "non-integral sampling factors"; return false; }
 
   // upsample each component to full resolution (jdsample.c fancy h2v1 / h2v2, else replicate)
   const int nc = (int)comps.size();
