@@ -161,6 +161,10 @@ def test_obj_short_faces_and_mixed_normals(host_device, tmp_path):
     s = yrt.Session(["-i", str(f), "-size", "16", "16"], device=host_device)
     assert host_device.scene_info(s.info()["scene"])["numTriangles"] == 1
     s.close()
+    h = tmp_path / "stray_cr.obj"  # a '\r' inside a face line once looped forever (fuzz finding)
+    h.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2\r 3\n")
+    with pytest.raises(RuntimeError, match="malformed face"):
+        yrt.Session(["-i", str(h), "-size", "16", "16"], device=host_device)
     g = tmp_path / "mixed.obj"
     g.write_text("v 0 0 0\nv 1 0 0\nv 0 1 0\nv 1 1 0\nvn 0 0 1\nf 1//1 2//1 3//1\nf 2 4 3\n")
     with pytest.raises(RuntimeError, match="normals"):

@@ -54,6 +54,9 @@ struct GpuCtx {
     hipStream_t stream = nullptr;
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
+#if YRT_SHADE_SORT_EXP
+    DevBuf sortKeys, sortVals, sortKeysOut, sortValsOut, sortTemp;
+#endif
     int64_t pathCap = 0, shadowCap = 0;
     // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
     // copy of the counters (written by the stream after the batch's last trace), the event
@@ -899,7 +902,24 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                     pb.segCap, st);
         EvPair e2{};
         if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
+#if YRT_SHADE_SORT_EXP
+        PathBuffers pbs = pb;
+        if (d > 0 && !getenv("YRT_NO_SHADE_SORT")) {
+          const int n = pb.segCap * YRT_QSEGS;
+          L.sortKeys.alloc((size_t)n * 4);
+          L.sortVals.alloc((size_t)n * 4);
+          L.sortKeysOut.alloc((size_t)n * 4);
+          L.sortValsOut.alloc((size_t)n * 4);
+          const size_t tb = shade_sort_temp_bytes(n);
+          L.sortTemp.alloc(std::max<size_t>(tb, 16));
+          launch_shade_sort(pb, d, n, L.sortKeys.as<int>(), L.sortVals.as<int>(), L.sortKeysOut.as<int>(),
+                            L.sortValsOut.as<int>(), L.sortTemp.p, tb, st);
+          pbs.shadePerm = L.sortValsOut.as<int>();
+        }
+        launch_shade(lsv, fv, pbs, bi, d, G.materialMask, st);
+#else
         launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
+#endif
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (numDirect > 0) {
           EvPair e3{};

@@ -593,8 +593,12 @@ struct OBJLoader {
         t = skipSep(t + 1);
         std::vector<OVertex> face;
         while (t[0]) {
+          const char* t0 = t;
           face.push_back(getInt3(t));
           t = skipSep(t);
+          // a separator getInt3 does not consume (a stray '\r' inside the line) would leave t
+          // in place and grow the face without bound (mutation fuzz finding)
+          if (t == t0) throw std::runtime_error("OBJ: malformed face line");
         }
         curGroup.push_back(face);
       } else if (!strncmp(t, "usemtl", 6) && sep(t[6])) {

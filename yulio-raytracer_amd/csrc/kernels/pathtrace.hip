@@ -20,6 +20,9 @@
 #include <set>
 
 #include "yrt_kernels.h"
+#if YRT_SHADE_SORT_EXP
+#include <hipcub/hipcub.hpp>
+#endif
 #include "yrt_shade.h"
 #include "yrt_traverse.h"
 
@@ -1379,7 +1382,11 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const unsigned ql = (unsigned)base + threadIdx.x;
     const bool active = (int)ql < n;
+#if YRT_SHADE_SORT_EXP
+    const int q = !active ? 0 : (pb.shadePerm && depthLevel > 0) ? pb.shadePerm[ql] : qmap_phys(qm, pb.segCap, ql);
+#else
     const int q = active ? qmap_phys(qm, pb.segCap, ql) : 0;
+#endif
     const int oseg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
     unsigned* nextCount = pb.counters + qcounter_index(depthLevel + 1, 0, oseg);
     unsigned* shadowCount = pb.counters + qcounter_index(depthLevel, 1, oseg);
@@ -1926,6 +1933,39 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
     }
   }
 }
+
+#if YRT_SHADE_SORT_EXP
+__global__ __launch_bounds__(YRT_BLOCK) void k_shade_sort_keys(const unsigned* __restrict__ counts, int segCap,
+                                                                const float4* __restrict__ hit, int n,
+                                                                int* __restrict__ keys, int* __restrict__ vals) {
+  __shared__ QMap qm;
+  qmap_load(qm, counts, YRT_QSEGS);
+  const unsigned total = qm.pre[YRT_QSEGS];
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n; i += gridDim.x * blockDim.x) {
+    int key = (1 << 18) - 1, q = -1;
+    if (i < total) {
+      q = qmap_phys(qm, segCap, i);
+      const int tri = __float_as_int(hit[q].w);
+      key = tri >= 0 && tri < (1 << 18) - 1 ? tri : (1 << 18) - 1;
+    }
+    keys[i] = key;
+    vals[i] = q;
+  }
+}
+size_t shade_sort_temp_bytes(int n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int*)nullptr, (int*)nullptr, (const int*)nullptr,
+                                           (int*)nullptr, n, 0, 18);
+  return bytes;
+}
+void launch_shade_sort(const PathBuffers& pb, int depth, int n, int* keys, int* vals, int* keysOut, int* valsOut,
+                       void* temp, size_t tempBytes, hipStream_t s) {
+  hipLaunchKernelGGL(k_shade_sort_keys, dim3(grid_for(n, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s,
+                     pb.counters + qcounter_index(depth, 0, 0), pb.segCap, pb.hit, n, keys, vals);
+  if (hipcub::DeviceRadixSort::SortPairs(temp, tempBytes, keys, keysOut, vals, valsOut, n, 0, 18, s) != hipSuccess)
+    fprintf(stderr, "yrt: shade sort failed\n");
+}
+#endif
 
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {
   hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK),

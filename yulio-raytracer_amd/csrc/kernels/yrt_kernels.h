@@ -112,6 +112,11 @@ struct PathBuffers {
   // so the sum is deterministic and in the reference's order; k_shadow_resolve is not
   // launched. 0: sOcc + shFirst + k_shadow_resolve (several lights, light order kept).
   int fuseShadow;
+#if YRT_SHADE_SORT_EXP
+  // experiment (round 5): k_shade at depth >= 1 visits its queue in the order of
+  // this permutation (queue slots sorted by hit triangle id), see launch_shade_sort
+  const int* shadePerm = nullptr;
+#endif
 };
 
 // Fused shadow resolve: sContrib.w = path id (bits) whose pathL receives the contribution.
@@ -176,6 +181,13 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
                   unsigned materialMask, hipStream_t s);
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
+#if YRT_SHADE_SORT_EXP
+// the closest queue entering `depth` sorted by hit triangle id (misses last): vals_out[i] is the
+// physical slot of the i-th entry; n = capacity entries are sorted (the count is device-side)
+size_t shade_sort_temp_bytes(int n);
+void launch_shade_sort(const PathBuffers& pb, int depth, int n, int* keys, int* vals, int* keysOut, int* valsOut,
+                       void* temp, size_t tempBytes, hipStream_t s);
+#endif
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
