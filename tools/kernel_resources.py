@@ -23,9 +23,11 @@ def main():
         for k, v in env.items():
             t = t.replace(f"$({k})", v)
         return t
-    cmd = ["/opt/rocm/bin/hipcc"] + expand(hip.group(1)).split() + sys.argv[1:] + [
+    cmd = ["/opt/rocm/bin/hipcc"] + expand(hip.group(1)).split() + [a for a in sys.argv[1:] if a != "--raw"] + [
         "-Rpass-analysis=kernel-resource-usage", "-c", "csrc/kernels/pathtrace.hip", "-o", "/tmp/kr.o"]
     out = subprocess.run(cmd, cwd=PKG, capture_output=True, text=True).stderr
+    if "--raw" in sys.argv:
+        print(out)
     rows, cur = [], None
     for line in out.splitlines():
         m = re.search(r"Function Name: (\S+)", line)

@@ -54,9 +54,7 @@ struct GpuCtx {
     hipStream_t stream = nullptr;
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
-#if YRT_SHADE_SORT_EXP
-    DevBuf sortKeys, sortVals, sortKeysOut, sortValsOut, sortTemp;
-#endif
+    DevBuf orderKeys, order;  // the shading order's bin keys and slot permutation (launch_shade_order)
     int64_t pathCap = 0, shadowCap = 0;
     // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
     // copy of the counters (written by the stream after the batch's last trace), the event
@@ -71,6 +69,7 @@ struct GpuCtx {
       int64_t tiles = 0;
       int64_t seq = 0;
       bool fused = false;  // depth 0 ran as k_trace's camera-ray instantiation
+      bool compact = false;  // ... with its hits compacted (the depth-0 queue count = its hits)
     };
     static constexpr int kPendDepth = 1;
     Pend pend[kPendDepth];
@@ -157,6 +156,8 @@ struct GpuCtx {
       }
       L.hit.alloc(Q * 16);
       L.pathL.alloc(Q * 16);
+      L.orderKeys.alloc(Q * 2);
+      L.order.alloc(Q * 4);
       L.pathCap = Q;
     }
     const int64_t S = Q * std::max(1, numLights);
@@ -709,15 +710,18 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // the capture frame (roofline accounting) reads batch 0's queues synchronously: one lane
     const int nl = captureMax > 0 ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(g.numLanes, numBatches));
     const int levels = rp.maxDepth + 1;
-    // the queue counters, then two words: the camera rays a fused depth 0 traced and how many
-    // of them hit (PrimaryRays::traced)
-    const size_t counterWords = qcounter_words(levels) + 2;
-    const size_t tracedWord = counterWords - 2, hitsWord = counterWords - 1;
+    // the queue counters, then one word: the camera rays a fused depth 0 traced
+    // (PrimaryRays::traced)
+    const size_t counterWords = qcounter_words(levels) + 1;
+    const size_t tracedWord = counterWords - 1;
+    // after them the shading order's bin counts (cleared with the counters, and by each scan)
+    // and bin cursors
+    const size_t binWords = 2 * (YRT_SHADE_BINS + 1);
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
       GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), numDirect, G.hasMotion);
-      L.counters.alloc(counterWords * sizeof(unsigned));
+      L.counters.alloc((counterWords + binWords) * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
       for (GpuCtx::Lane::Pend& Pd : L.pend) {
         if (Pd.hcWords < counterWords) {
@@ -783,10 +787,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           nc += Pd.hc[qcounter_index(d, 0, k)];
           ns += Pd.hc[qcounter_index(d, 1, k)];
         }
-        if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
+        if (d == 0 && Pd.fused && Pd.compact && Pd.hc[tracedWord] > 0) {
           if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
           auto& acc = g.missFrac[G.serial];
-          acc.first += (double)Pd.hc[tracedWord] - (double)Pd.hc[hitsWord];
+          acc.first += (double)Pd.hc[tracedWord] - nc;  // a compact depth 0 queues its hits only
           acc.second += (double)Pd.hc[tracedWord];
           missEst = acc.first / acc.second;
         }
@@ -818,6 +822,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // waves/SIMD and its hits are appended scattered, profiles/r04/ab_r04d.txt), so a batch is
     // fused while the scene's measured miss share (missFrac, over its fused batches so far) is at
     // least YRT_PRIMARY_MISS (default 0.5) or unknown. YRT_PRIMARY=0: never, 2: always.
+    // k_shade at depth >= YRT_SHADE_ORDER_DEPTH in the shading order (launch_shade_order);
+    // YRT_SHADE_ORDER=0: queue order (the invariance tests compare the two)
+    const bool shadeOrder = !getenv("YRT_SHADE_ORDER") || atoi(getenv("YRT_SHADE_ORDER")) != 0;
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
@@ -865,7 +872,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.tileStride = count;
       bi.tileOffset = index;
       bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
-      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
+      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, (counterWords + binWords / 2) * sizeof(unsigned), st));
       // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
       // YRT_PRIMARY_IDENTITY=1 for the scenes whose rays mostly hit) or k_raygen otherwise
       const bool compactBatch = primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss));
@@ -902,24 +909,14 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                     pb.segCap, st);
         EvPair e2{};
         if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
-#if YRT_SHADE_SORT_EXP
         PathBuffers pbs = pb;
-        if (d > 0 && !getenv("YRT_NO_SHADE_SORT")) {
-          const int n = pb.segCap * YRT_QSEGS;
-          L.sortKeys.alloc((size_t)n * 4);
-          L.sortVals.alloc((size_t)n * 4);
-          L.sortKeysOut.alloc((size_t)n * 4);
-          L.sortValsOut.alloc((size_t)n * 4);
-          const size_t tb = shade_sort_temp_bytes(n);
-          L.sortTemp.alloc(std::max<size_t>(tb, 16));
-          launch_shade_sort(pb, d, n, L.sortKeys.as<int>(), L.sortVals.as<int>(), L.sortKeysOut.as<int>(),
-                            L.sortValsOut.as<int>(), L.sortTemp.p, tb, st);
-          pbs.shadePerm = L.sortValsOut.as<int>();
+        pbs.rayByPath = d == 0 && fusedBatch ? 1 : 0;
+        if (d >= YRT_SHADE_ORDER_DEPTH && shadeOrder) {
+          launch_shade_order(pb, d, sv.numTris, L.orderKeys.as<uint16_t>(), L.counters.as<unsigned>() + counterWords,
+                             L.order.as<int>(), st);
+          pbs.shadeOrder = L.order.as<int>();
         }
         launch_shade(lsv, fv, pbs, bi, d, G.materialMask, st);
-#else
-        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
-#endif
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (numDirect > 0) {
           EvPair e3{};
@@ -941,6 +938,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipEventRecord(Pd.done, st));
       Pd.tiles = bi.numPixels / 256;
       Pd.fused = fusedBatch;
+      Pd.compact = fusedBatch && compactBatch;
       Pd.seq = batch;
       L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,

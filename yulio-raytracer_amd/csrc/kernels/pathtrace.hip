@@ -20,9 +20,6 @@
 #include <set>
 
 #include "yrt_kernels.h"
-#if YRT_SHADE_SORT_EXP
-#include <hipcub/hipcub.hpp>
-#endif
 #include "yrt_shade.h"
 #include "yrt_traverse.h"
 
@@ -34,6 +31,17 @@ namespace yrt {
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+#ifndef YRT_MBCNT
+#define YRT_MBCNT 1
+#endif
+// set bits of a wave mask below this lane (v_mbcnt: no per-lane mask register kept live)
+__device__ __forceinline__ unsigned lanes_below(unsigned long long m) {
+#if YRT_MBCNT
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+#else
+  return (unsigned)__popcll(m & ((1ull << __lane_id()) - 1ull));
+#endif
+}
 
 // Reserve k slots (k >= 0 per lane) in *counter; returns this lane's first slot.
 // Every lane of the wave must call it (no divergent callers).
@@ -549,23 +557,20 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // refill (or at the wave's end), instead of at every accepted hit; q = -1: nothing to store
   float bestDen = 1.f;
   q = -1;
-  const unsigned long long ltMask = (1ull << lane) - 1ull;
-  // PRIM: a finished camera ray (q = its path id) — a hit is appended with its records to the
-  // depth-0 queue segment of its path id's 64-group (one atomic per segment among the storing
-  // lanes), a miss gets the environment's radiance
-  unsigned primTraced = 0, primHits = 0;  // camera rays this lane traced, and hit
+  // PRIM: a finished camera ray (q = its path id) — a hit is appended to the depth-0 queue
+  // segment of its path id's 64-group (one atomic per segment among the storing lanes) as its
+  // path id and hit record; a miss keeps the environment's radiance that k_fill_paths wrote
+  // before the launch (no value carried through the loop for it). The ray itself was stored at
+  // its path id when it was generated (k_shade reads depth-0 rays by path id,
+  // PathBuffers::rayByPath), so no ray is held for the store.
   auto prim_store = [&]() {
     const bool hitp = best.tri >= 0;
-    primHits += hitp ? 1u : 0u;
     if constexpr (kIdentity) {
       // identity layout: every path keeps its own slot, misses included (k_shade shades them)
       pr.qPath[q] = q;
-      pr.qOrg[q] = ro;
-      pr.qDir[q] = rd;
       hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
       return;
     }
-    if (!hitp) pr.pathL[q] = pr.missL;
     const int seg = qseg_of((unsigned)q);
     unsigned long long m = ballot(hitp);
     while (m) {
@@ -576,10 +581,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       if (lane == l0) base = atomicAdd(pr.counts + (size_t)seg0 * YRT_QCSTRIDE, (unsigned)__popcll(sub));
       base = (unsigned)__builtin_amdgcn_readlane((int)base, l0);
       if (hitp && seg == seg0) {
-        const unsigned slot = (unsigned)seg0 * (unsigned)pr.segCap + base + (unsigned)__popcll(sub & ltMask);
+        const unsigned slot = (unsigned)seg0 * (unsigned)pr.segCap + base + lanes_below(sub);
         pr.qPath[slot] = q;
-        pr.qOrg[slot] = ro;
-        pr.qDir[slot] = rd;
         hitOut[slot] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
       }
       m &= ~sub;
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     YRT_PROF(1, 64 - nIdle);
     if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
       if (next < end) {
-        const unsigned li = next + (unsigned)__popcll(idle & ltMask);
+        const unsigned li = next + lanes_below(idle);
         if (!has) {
           if (!ANY && q >= 0) YRT_STORE_HIT();
           if (li < end) {
@@ -642,8 +645,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                 }
                 ro = make_float4(o3.x, o3.y, o3.z, 0.f);
                 rd = make_float4(d3.x, d3.y, d3.z, __int_as_float(0x7f800000));
+                pr.qOrg[p] = ro;
+                pr.qDir[p] = rd;
                 q = p;
-                primTraced += 1;
               } else {
                 pr.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);  // not a pixel of the image
                 if constexpr (kIdentity) {
@@ -688,13 +692,23 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       } else if (nIdle == 64) {
         if (!ANY && q >= 0) YRT_STORE_HIT();
         if constexpr (PRIM) {
-          unsigned t = primTraced, hc = primHits;
-          for (int o = 32; o > 0; o >>= 1) {
-            t += __shfl_xor(t, o, 64);
-            hc += __shfl_xor(hc, o, 64);
+          // the camera rays this wave traced: the valid path ids of its chunk (the refill's
+          // test again, after the loop, so that no count is carried through it)
+          const YRT_CONST GpuRenderParams& rp = const_ref(pr.fv.rp);
+          unsigned t = 0;
+          if (rp.maxDepth > 0 && !(1.0f < rp.minContribution)) {
+            for (unsigned b = gw * chunk; b < end; b += 64) {
+              const unsigned p = b + (unsigned)lane;
+              bool v = false;
+              if (p < end) {
+                const int smp = fastdiv((int)p, pr.bi.divPixels);
+                int x, y, f;
+                v = batch_pixel(rp, pr.bi, (int)p - smp * pr.bi.numPixels, x, y, f);
+              }
+              t += (unsigned)__popcll(ballot(v));
+            }
           }
           if (lane == 0 && t) atomicAdd(pr.traced, t);
-          if (lane == 0 && hc) atomicAdd(pr.traced + 1, hc);
         }
 #ifdef YRT_PROFILE
         if (lane == 0)
@@ -1382,11 +1396,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const unsigned ql = (unsigned)base + threadIdx.x;
     const bool active = (int)ql < n;
-#if YRT_SHADE_SORT_EXP
-    const int q = !active ? 0 : (pb.shadePerm && depthLevel > 0) ? pb.shadePerm[ql] : qmap_phys(qm, pb.segCap, ql);
-#else
-    const int q = active ? qmap_phys(qm, pb.segCap, ql) : 0;
-#endif
+    const int q = !active ? 0 : pb.shadeOrder ? pb.shadeOrder[ql] : qmap_phys(qm, pb.segCap, ql);
     const int oseg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
     unsigned* nextCount = pb.counters + qcounter_index(depthLevel + 1, 0, oseg);
     unsigned* shadowCount = pb.counters + qcounter_index(depthLevel, 1, oseg);
@@ -1438,8 +1448,10 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     // reads the direction only for an emitting environment light whose Le depends on it, and
     // neither the origin nor the sample record unless it looks up the backplate (a hit issues
     // these loads beside its shading record's, off its dependent chain)
+    // a fused depth 0 stored its rays at their path ids (PathBuffers::rayByPath)
+    const int rq = depthLevel == 0 && pb.rayByPath ? path : q;
     if (active && (isHit || sv.numEnvDir > 0)) {
-      const float4 d = pb.qDir[cur][q];
+      const float4 d = pb.qDir[cur][rq];
       dir = v3(d.x, d.y, d.z);
       wo = -dir;
     }
@@ -1481,7 +1493,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       const int gid = __float_as_int(h.w);
       const float4* tsr = (const float4*)(sv.triShade + gid);
       const float4 r0 = tsr[0];
-      const float4 o = pb.qOrg[cur][q];
+      const float4 o = pb.qOrg[cur][rq];
       org = v3(o.x, o.y, o.z);
       rec = fv.pixelSets[pixelId] * rp.spp + s;
       g = __float_as_int(r0.w);  // geometry id rides in the shading record
@@ -1844,8 +1856,17 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
                        segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr, PrimaryRays{});
 }
 
+// every path's radiance set to a depth-0 miss's (compact fused depth 0: the trace writes only
+// the hits' queue records and the paths outside the image; k_shade overwrites the hits' radiance)
+__global__ __launch_bounds__(256) void k_fill_paths(float4* __restrict__ pathL, long long n, float4 v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    pathL[i] = v;
+}
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
+  if (!pr.identity)
+    hipLaunchKernelGGL(k_fill_paths, dim3(grid_for(pr.numPaths, 256, 8192)), dim3(256), 0, s, pr.pathL, pr.numPaths,
+                       pr.missL);
 #define YRT_LAUNCH_PRIM(k)                                                                                 \
   hipLaunchKernelGGL((k_trace<false, false, k>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr, \
                      (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,      \
@@ -1934,38 +1955,107 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
   }
 }
 
-#if YRT_SHADE_SORT_EXP
-__global__ __launch_bounds__(YRT_BLOCK) void k_shade_sort_keys(const unsigned* __restrict__ counts, int segCap,
-                                                                const float4* __restrict__ hit, int n,
-                                                                int* __restrict__ keys, int* __restrict__ vals) {
+// ---------------------------------------------------------------- shading order
+// Counting sort of the live queue slots by a bin of the hit triangle id (YRT_SHADE_BINS ranges
+// of the id, misses in bin YRT_SHADE_BINS), see launch_shade_order. Both passes split the
+// logical range [0, n) into the same contiguous per-block chunks, so a block's scatter
+// reproduces its own histogram; within a bin the order is the blocks' order.
+#define YRT_ORDER_BLOCK 512
+#define YRT_ORDER_GRID 512
+__device__ __forceinline__ void order_chunk(unsigned n, unsigned& lo, unsigned& hi) {
+  const unsigned chunk = (n + gridDim.x - 1) / gridDim.x;
+  lo = min(n, blockIdx.x * chunk);
+  hi = min(n, lo + chunk);
+}
+__global__ __launch_bounds__(YRT_ORDER_BLOCK) void k_order_count(const unsigned* __restrict__ counts, int segCap,
+                                                                 const float4* __restrict__ hit, float binScale,
+                                                                 uint16_t* __restrict__ keys,
+                                                                 unsigned* __restrict__ binCount) {
   __shared__ QMap qm;
-  qmap_load(qm, counts, YRT_QSEGS);
-  const unsigned total = qm.pre[YRT_QSEGS];
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < (unsigned)n; i += gridDim.x * blockDim.x) {
-    int key = (1 << 18) - 1, q = -1;
-    if (i < total) {
-      q = qmap_phys(qm, segCap, i);
-      const int tri = __float_as_int(hit[q].w);
-      key = tri >= 0 && tri < (1 << 18) - 1 ? tri : (1 << 18) - 1;
+  __shared__ unsigned hist[YRT_SHADE_BINS + 1];
+  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x) hist[k] = 0;
+  qmap_load(qm, counts, YRT_QSEGS);  // barrier inside
+  unsigned lo, hi;
+  order_chunk(qm.pre[YRT_QSEGS], lo, hi);
+  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int q = qmap_phys(qm, segCap, i);
+    const int tri = __float_as_int(hit[q].w);
+    const int key = tri < 0 ? YRT_SHADE_BINS : min(YRT_SHADE_BINS - 1, (int)((float)tri * binScale));
+    keys[i] = (uint16_t)key;
+    atomicAdd(&hist[key], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x)
+    if (hist[k]) atomicAdd(binCount + k, hist[k]);
+}
+// one block: binCursor = exclusive prefix of binCount, binCount cleared for the next depth
+__global__ __launch_bounds__(1024) void k_order_scan(unsigned* __restrict__ binCount, unsigned* __restrict__ binCursor) {
+  constexpr int kPer = (YRT_SHADE_BINS + 1 + 1023) / 1024;
+  __shared__ unsigned waveSum[16];
+  const int t = threadIdx.x;
+  unsigned c[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = t * kPer + j;
+    c[j] = k <= YRT_SHADE_BINS ? binCount[k] : 0u;
+    sum += c[j];
+  }
+  // inclusive scan of the per-thread sums: within the wave, then over the waves
+  unsigned inc = sum;
+  const int lane = t & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) waveSum[t >> 6] = inc;
+  __syncthreads();
+  unsigned waveBase = 0;
+  for (int w = 0; w < (t >> 6); ++w) waveBase += waveSum[w];
+  unsigned run = waveBase + inc - sum;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int k = t * kPer + j;
+    if (k <= YRT_SHADE_BINS) {
+      binCursor[k] = run;
+      binCount[k] = 0u;
     }
-    keys[i] = key;
-    vals[i] = q;
+    run += c[j];
   }
 }
-size_t shade_sort_temp_bytes(int n) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int*)nullptr, (int*)nullptr, (const int*)nullptr,
-                                           (int*)nullptr, n, 0, 18);
-  return bytes;
+__global__ __launch_bounds__(YRT_ORDER_BLOCK) void k_order_scatter(const unsigned* __restrict__ counts, int segCap,
+                                                                   const uint16_t* __restrict__ keys,
+                                                                   unsigned* __restrict__ binCursor,
+                                                                   int* __restrict__ order) {
+  __shared__ QMap qm;
+  __shared__ unsigned pos[YRT_SHADE_BINS + 1];
+  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x) pos[k] = 0;
+  qmap_load(qm, counts, YRT_QSEGS);  // barrier inside
+  unsigned lo, hi;
+  order_chunk(qm.pre[YRT_QSEGS], lo, hi);
+  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&pos[keys[i]], 1u);
+  __syncthreads();
+  // this block's range of each bin
+  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x)
+    if (pos[k]) pos[k] = atomicAdd(binCursor + k, pos[k]);
+  __syncthreads();
+  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const unsigned at = atomicAdd(&pos[keys[i]], 1u);
+    order[at] = qmap_phys(qm, segCap, i);
+  }
 }
-void launch_shade_sort(const PathBuffers& pb, int depth, int n, int* keys, int* vals, int* keysOut, int* valsOut,
-                       void* temp, size_t tempBytes, hipStream_t s) {
-  hipLaunchKernelGGL(k_shade_sort_keys, dim3(grid_for(n, YRT_BLOCK, 16384)), dim3(YRT_BLOCK), 0, s,
-                     pb.counters + qcounter_index(depth, 0, 0), pb.segCap, pb.hit, n, keys, vals);
-  if (hipcub::DeviceRadixSort::SortPairs(temp, tempBytes, keys, keysOut, vals, valsOut, n, 0, 18, s) != hipSuccess)
-    fprintf(stderr, "yrt: shade sort failed\n");
+void launch_shade_order(const PathBuffers& pb, int depth, int numTris, uint16_t* keys, unsigned* binWords, int* order,
+                        hipStream_t s) {
+  const unsigned* counts = pb.counters + qcounter_index(depth, 0, 0);
+  const float binScale = (float)YRT_SHADE_BINS / (float)(numTris > 0 ? numTris : 1);
+  unsigned* binCount = binWords;
+  unsigned* binCursor = binWords + YRT_SHADE_BINS + 1;
+  hipLaunchKernelGGL(k_order_count, dim3(YRT_ORDER_GRID), dim3(YRT_ORDER_BLOCK), 0, s, counts, pb.segCap, pb.hit,
+                     binScale, keys, binCount);
+  hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(1024), 0, s, binCount, binCursor);
+  hipLaunchKernelGGL(k_order_scatter, dim3(YRT_ORDER_GRID), dim3(YRT_ORDER_BLOCK), 0, s, counts, pb.segCap, keys,
+                     binCursor, order);
 }
-#endif
 
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {
   hipLaunchKernelGGL(k_shadow_resolve, dim3(grid_for(pb.capacity, YRT_BLOCK, 8192)), dim3(YRT_BLOCK),
