@@ -360,45 +360,6 @@ def test_fused_primary_invariance(gpu_device, monkeypatch, which):
         assert out[0][1:] == o[1:]
 
 
-@pytest.mark.parametrize("which", ["C3", "materials", "C5"])
-def test_shade_order_invariance(gpu_device, monkeypatch, which):
-    """k_shade through the shading order (queue slots grouped by hit triangle, depth >= 1,
-    launch_shade_order) against queue order (YRT_SHADE_ORDER=0): bit-identical frames and the same
-    query counts. Every path's vertex depends on its own record only, so the order may change
-    which wave shades it and where its rays land in the next queue, never the result: C3 (one
-    light, fused shadow adds) over several batches on both lanes, the materials scene (every BRDF,
-    several lights: the shadow-resolve pass over permuted slots), the C5 stand-in cube (Collada
-    materials, a thin light sphere)."""
-    from test_materials_lights import ARGS as MAT_ARGS
-    from yrt import frederick
-    out = []
-    for order in ("0", "1"):
-        monkeypatch.setenv("YRT_SHADE_ORDER", order)
-        gpu_device.set_batch_capacity(256 * 16 * 5)
-        try:
-            if which == "C3":
-                s = _session(gpu_device, c3_args(96, 4))
-                img = [s.render()]
-            elif which == "materials":
-                s = _session(gpu_device, MAT_ARGS + ["-size", "96", "72", "-spp", "8", "-depth", "6",
-                                                     "-fb", "RGB_FLOAT32"])
-                img = [s.render()]
-            else:
-                s = _session(gpu_device, ["-fprCollada", "-faceCullingMode", "default", "-i",
-                                          str(frederick.write_dae()), "-stereo", "-size", "48", "48", "-spp", "4",
-                                          "-fb", "RGB_FLOAT32", "-tMaxShadowRay", "120", "-ambientlight", "0.83",
-                                          "0.95", "0.98", "-depth", "10", "-toeIn"])
-                img = s.render_scene_cube(0)
-            st = gpu_device.render_stats()
-        finally:
-            gpu_device.set_batch_capacity(64 << 20)
-        s.close()
-        out.append((img, st["raysClosest"], st["raysShadow"]))
-    for a, b in zip(out[0][0], out[1][0]):
-        assert np.array_equal(a, b)
-    assert out[0][1:] == out[1][1:]
-
-
 def test_lanes_invariance(monkeypatch):
     """Batches spread over one or two lanes (streams) give bit-identical frames."""
     imgs = []

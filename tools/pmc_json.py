@@ -26,9 +26,12 @@ from collections import defaultdict
 from pathlib import Path
 
 SIMDS, XCDS = 256 * 4, 8
-KERNELS = {"k_trace<false>": "k_trace<false", "k_trace<true>": "k_trace<true", "k_occluded": "k_occluded", "k_shade": "k_shade", "k_raygen": "k_raygen",
-           "k_shadow_resolve": "k_shadow_resolve", "k_resolve_pixels": "k_resolve_pixels",
-           "k_valu_calib": "k_valu_calib"}
+# k_occluded (batch E) and k_order_* (batch H's shading-order variant): rejected experiments,
+# kept here so that their committed PMC records can be regenerated from the variant builds
+KERNELS = {"k_trace<false>": "k_trace<false", "k_trace<true>": "k_trace<true", "k_occluded": "k_occluded",
+           "k_shade": "k_shade<", "k_raygen": "k_raygen", "k_order_count": "k_order_count",
+           "k_order_scatter": "k_order_scatter", "k_shadow_resolve": "k_shadow_resolve",
+           "k_resolve_pixels": "k_resolve_pixels", "k_fill_paths": "k_fill_paths", "k_valu_calib": "k_valu_calib"}
 
 
 def per_dispatch(dirs):
@@ -38,8 +41,8 @@ def per_dispatch(dirs):
         for f in Path(d).rglob("*counter_collection.csv"):
             for row in csv.DictReader(open(f)):
                 name = row.get("Kernel_Name", "")
-                # the fused depth-0 instantiations (k_trace<false, false, false, 1..4>) apart
-                prim = re.search(r"k_trace<false, \w+, \w+, [1-4]>", name) is not None
+                # the fused depth-0 instantiations (k_trace<false, false, 1..4>) apart
+                prim = re.search(r"k_trace<false, \w+, [1-4]>", name) is not None
                 for k, tag in KERNELS.items():
                     if k == "k_trace<false>" and prim:
                         k = "k_trace<false> depth 0 fused"

@@ -178,6 +178,9 @@ struct GpuRenderParams {
   // the job is tile t % tilesPerFrame of frame t / tilesPerFrame (numTilesX * numTilesY each)
   int32_t numFrames, tilesPerFrame, pad;
   FastDiv divTilesX, divTilesPerFrame;  // fastdiv_make(numTilesX), fastdiv_make(tilesPerFrame)
+  // radiance of a camera ray that misses, for the fused depth 0 (PrimaryRays): the sum over the
+  // environment lights of 1 * L, as k_shade's depth-0 miss branch adds it (ambient lights only)
+  float missL[4];
 };
 
 // Camera (cameras/pinholecamera.h:15-21, cameras/StereoCubeCamera.h:16-65).

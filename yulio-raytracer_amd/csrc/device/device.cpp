@@ -54,7 +54,6 @@ struct GpuCtx {
     hipStream_t stream = nullptr;
     DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
-    DevBuf orderKeys, order;  // the shading order's bin keys and slot permutation (launch_shade_order)
     int64_t pathCap = 0, shadowCap = 0;
     // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
     // copy of the counters (written by the stream after the batch's last trace), the event
@@ -156,8 +155,6 @@ struct GpuCtx {
       }
       L.hit.alloc(Q * 16);
       L.pathL.alloc(Q * 16);
-      L.orderKeys.alloc(Q * 2);
-      L.order.alloc(Q * 4);
       L.pathCap = Q;
     }
     const int64_t S = Q * std::max(1, numLights);
@@ -614,6 +611,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
   sv.numDirectLights = (int)g.hDirect.size();
   const int numDirect = sv.numDirectLights;
 
+  // a fused depth 0's miss radiance (PrimaryRays)
+  for (int k = 0; k < 4; ++k) rp.missL[k] = 0.f;
+  for (int j : G.hEnvLights) {
+    const float* Le = G.hLights[j].L;
+    for (int k = 0; k < 3; ++k) rp.missL[k] = rp.missL[k] + 1.0f * Le[k];
+  }
   g.dRp.alloc(sizeof(rp));
   g.hCams.resize(nf);
   for (int k = 0; k < nf; ++k) g.hCams[k] = C[k]->cam;
@@ -714,14 +717,11 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // (PrimaryRays::traced)
     const size_t counterWords = qcounter_words(levels) + 1;
     const size_t tracedWord = counterWords - 1;
-    // after them the shading order's bin counts (cleared with the counters, and by each scan)
-    // and bin cursors
-    const size_t binWords = 2 * (YRT_SHADE_BINS + 1);
     g.dAccu.alloc((size_t)nf * W * H * 16);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
       GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), numDirect, G.hasMotion);
-      L.counters.alloc((counterWords + binWords) * sizeof(unsigned));
+      L.counters.alloc(counterWords * sizeof(unsigned));
       L.spill.alloc(YRT_TRACE_SPILL_INTS * sizeof(int));
       for (GpuCtx::Lane::Pend& Pd : L.pend) {
         if (Pd.hcWords < counterWords) {
@@ -822,9 +822,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // waves/SIMD and its hits are appended scattered, profiles/r04/ab_r04d.txt), so a batch is
     // fused while the scene's measured miss share (missFrac, over its fused batches so far) is at
     // least YRT_PRIMARY_MISS (default 0.5) or unknown. YRT_PRIMARY=0: never, 2: always.
-    // k_shade at depth >= YRT_SHADE_ORDER_DEPTH in the shading order (launch_shade_order);
-    // YRT_SHADE_ORDER=0: queue order (the invariance tests compare the two)
-    const bool shadeOrder = !getenv("YRT_SHADE_ORDER") || atoi(getenv("YRT_SHADE_ORDER")) != 0;
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
@@ -832,13 +829,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     const bool identityOk = rp.maxDepth > 0 && !(1.0f < rp.minContribution);
     bool allPinhole = true;
     for (int k = 0; k < nf; ++k) allPinhole &= g.hCams[k].type == CAM_PINHOLE;
-    float4 missL = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int j : G.hEnvLights) {
-      const float* Le = G.hLights[j].L;
-      missL.x = missL.x + 1.0f * Le[0];
-      missL.y = missL.y + 1.0f * Le[1];
-      missL.z = missL.z + 1.0f * Le[2];
-    }
     for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
       const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - first);
       if (R.stopFlag && R.stopFlag->load()) break;
@@ -872,7 +862,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.tileStride = count;
       bi.tileOffset = index;
       bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
-      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, (counterWords + binWords / 2) * sizeof(unsigned), st));
+      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
       // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
       // YRT_PRIMARY_IDENTITY=1 for the scenes whose rays mostly hit) or k_raygen otherwise
       const bool compactBatch = primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss));
@@ -893,7 +883,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           pr.pathL = pb.pathL;
           pr.counts = pb.counters + qcounter_index(0, 0, 0);
           pr.segCap = pb.segCap;
-          pr.missL = missL;
           pr.traced = pb.counters + tracedWord;
           pr.numPaths = (long long)bi.numPixels * spp;
           pr.pinholeOnly = allPinhole ? 1 : 0;
@@ -909,14 +898,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                     pb.segCap, st);
         EvPair e2{};
         if (kernelTiming) { e2 = {g.ev(), g.ev(), 2}; HIP_CHECK(hipEventRecord(e2.a, st)); }
-        PathBuffers pbs = pb;
-        pbs.rayByPath = d == 0 && fusedBatch ? 1 : 0;
-        if (d >= YRT_SHADE_ORDER_DEPTH && shadeOrder) {
-          launch_shade_order(pb, d, sv.numTris, L.orderKeys.as<uint16_t>(), L.counters.as<unsigned>() + counterWords,
-                             L.order.as<int>(), st);
-          pbs.shadeOrder = L.order.as<int>();
-        }
-        launch_shade(lsv, fv, pbs, bi, d, G.materialMask, st);
+        launch_shade(lsv, fv, pb, bi, d, G.materialMask, st);
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e2.b, st)); evs.push_back(e2); }
         if (numDirect > 0) {
           EvPair e3{};

@@ -31,16 +31,15 @@ namespace yrt {
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
-#ifndef YRT_MBCNT
-#define YRT_MBCNT 1
-#endif
+// 0.0f computed where it is used (volatile: not hoisted out of a loop)
+__device__ __forceinline__ float opaque_zero() {
+  float z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
 // set bits of a wave mask below this lane (v_mbcnt: no per-lane mask register kept live)
 __device__ __forceinline__ unsigned lanes_below(unsigned long long m) {
-#if YRT_MBCNT
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-#else
-  return (unsigned)__popcll(m & ((1ull << __lane_id()) - 1ull));
-#endif
 }
 
 // Reserve k slots (k >= 0 per lane) in *counter; returns this lane's first slot.
@@ -423,7 +422,8 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_TRACE_WAVES 6
 #endif
 #ifndef YRT_TRACE_WAVES_PRIM
-#define YRT_TRACE_WAVES_PRIM YRT_TRACE_WAVES  // the camera-ray (fused depth-0) instantiations
+// the camera-ray (fused depth-0) instantiations: register target of 5 waves/SIMD (96 VGPRs)
+#define YRT_TRACE_WAVES_PRIM 5
 #endif
 #ifndef YRT_TRACE_WAVES_ANY
 #define YRT_TRACE_WAVES_ANY YRT_TRACE_WAVES  // occupancy target of the shadow-ray instantiation
@@ -557,17 +557,24 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // refill (or at the wave's end), instead of at every accepted hit; q = -1: nothing to store
   float bestDen = 1.f;
   q = -1;
-  // PRIM: a finished camera ray (q = its path id) — a hit is appended to the depth-0 queue
-  // segment of its path id's 64-group (one atomic per segment among the storing lanes) as its
-  // path id and hit record; a miss keeps the environment's radiance that k_fill_paths wrote
-  // before the launch (no value carried through the loop for it). The ray itself was stored at
-  // its path id when it was generated (k_shade reads depth-0 rays by path id,
-  // PathBuffers::rayByPath), so no ray is held for the store.
+  // PRIM: a finished camera ray (q = its path id) — a hit is appended with its ray and hit
+  // record to the depth-0 queue segment of its path id's 64-group (one atomic per segment among
+  // the storing lanes); a miss gets the environment's radiance, loaded from the render
+  // parameters where it is stored (a value held in registers through the loop costs four of
+  // them). The camera rays traced are counted after the loop, no counter is carried through it.
   auto prim_store = [&]() {
     const bool hitp = best.tri >= 0;
+    if constexpr (!kIdentity) {
+      if (!hitp) {
+        const float* mL = pr.fv.rp->missL;
+        pr.pathL[q] = make_float4(mL[0], mL[1], mL[2], mL[3]);
+      }
+    }
     if constexpr (kIdentity) {
       // identity layout: every path keeps its own slot, misses included (k_shade shades them)
       pr.qPath[q] = q;
+      pr.qOrg[q] = ro;
+      pr.qDir[q] = rd;
       hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
       return;
     }
@@ -583,6 +590,8 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       if (hitp && seg == seg0) {
         const unsigned slot = (unsigned)seg0 * (unsigned)pr.segCap + base + lanes_below(sub);
         pr.qPath[slot] = q;
+        pr.qOrg[slot] = ro;
+        pr.qDir[slot] = rd;
         hitOut[slot] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
       }
       m &= ~sub;
@@ -645,15 +654,16 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                 }
                 ro = make_float4(o3.x, o3.y, o3.z, 0.f);
                 rd = make_float4(d3.x, d3.y, d3.z, __int_as_float(0x7f800000));
-                pr.qOrg[p] = ro;
-                pr.qDir[p] = rd;
                 q = p;
               } else {
-                pr.pathL[p] = make_float4(0.f, 0.f, 0.f, 0.f);  // not a pixel of the image
+                // a zero made here: a constant zero vector is hoisted out of the loop and held in
+                // four registers (spilled at a 5-wave register target)
+                const float z = opaque_zero();
+                pr.pathL[p] = make_float4(z, z, z, z);  // not a pixel of the image
                 if constexpr (kIdentity) {
                   // its slot reads as a miss (k_shade's miss adds go to a pixel no resolve reads)
                   pr.qPath[p] = p;
-                  hitOut[p] = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+                  hitOut[p] = make_float4(z, z, z, __int_as_float(-1));
                 }
                 q = -1;
                 ro = make_float4(0.f, 0.f, 0.f, 1.f);  // tfar < tnear: nothing to traverse
@@ -1396,7 +1406,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const unsigned ql = (unsigned)base + threadIdx.x;
     const bool active = (int)ql < n;
-    const int q = !active ? 0 : pb.shadeOrder ? pb.shadeOrder[ql] : qmap_phys(qm, pb.segCap, ql);
+    const int q = active ? qmap_phys(qm, pb.segCap, ql) : 0;
     const int oseg = qseg_of((unsigned)base + (threadIdx.x & ~63u));
     unsigned* nextCount = pb.counters + qcounter_index(depthLevel + 1, 0, oseg);
     unsigned* shadowCount = pb.counters + qcounter_index(depthLevel, 1, oseg);
@@ -1448,10 +1458,8 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     // reads the direction only for an emitting environment light whose Le depends on it, and
     // neither the origin nor the sample record unless it looks up the backplate (a hit issues
     // these loads beside its shading record's, off its dependent chain)
-    // a fused depth 0 stored its rays at their path ids (PathBuffers::rayByPath)
-    const int rq = depthLevel == 0 && pb.rayByPath ? path : q;
     if (active && (isHit || sv.numEnvDir > 0)) {
-      const float4 d = pb.qDir[cur][rq];
+      const float4 d = pb.qDir[cur][q];
       dir = v3(d.x, d.y, d.z);
       wo = -dir;
     }
@@ -1493,7 +1501,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       const int gid = __float_as_int(h.w);
       const float4* tsr = (const float4*)(sv.triShade + gid);
       const float4 r0 = tsr[0];
-      const float4 o = pb.qOrg[cur][rq];
+      const float4 o = pb.qOrg[cur][q];
       org = v3(o.x, o.y, o.z);
       rec = fv.pixelSets[pixelId] * rp.spp + s;
       g = __float_as_int(r0.w);  // geometry id rides in the shading record
@@ -1856,17 +1864,8 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
                        segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr, PrimaryRays{});
 }
 
-// every path's radiance set to a depth-0 miss's (compact fused depth 0: the trace writes only
-// the hits' queue records and the paths outside the image; k_shade overwrites the hits' radiance)
-__global__ __launch_bounds__(256) void k_fill_paths(float4* __restrict__ pathL, long long n, float4 v) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    pathL[i] = v;
-}
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
-  if (!pr.identity)
-    hipLaunchKernelGGL(k_fill_paths, dim3(grid_for(pr.numPaths, 256, 8192)), dim3(256), 0, s, pr.pathL, pr.numPaths,
-                       pr.missL);
 #define YRT_LAUNCH_PRIM(k)                                                                                 \
   hipLaunchKernelGGL((k_trace<false, false, k>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr, \
                      (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,      \
@@ -1953,108 +1952,6 @@ void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& p
       break;
     }
   }
-}
-
-// ---------------------------------------------------------------- shading order
-// Counting sort of the live queue slots by a bin of the hit triangle id (YRT_SHADE_BINS ranges
-// of the id, misses in bin YRT_SHADE_BINS), see launch_shade_order. Both passes split the
-// logical range [0, n) into the same contiguous per-block chunks, so a block's scatter
-// reproduces its own histogram; within a bin the order is the blocks' order.
-#define YRT_ORDER_BLOCK 512
-#define YRT_ORDER_GRID 512
-__device__ __forceinline__ void order_chunk(unsigned n, unsigned& lo, unsigned& hi) {
-  const unsigned chunk = (n + gridDim.x - 1) / gridDim.x;
-  lo = min(n, blockIdx.x * chunk);
-  hi = min(n, lo + chunk);
-}
-__global__ __launch_bounds__(YRT_ORDER_BLOCK) void k_order_count(const unsigned* __restrict__ counts, int segCap,
-                                                                 const float4* __restrict__ hit, float binScale,
-                                                                 uint16_t* __restrict__ keys,
-                                                                 unsigned* __restrict__ binCount) {
-  __shared__ QMap qm;
-  __shared__ unsigned hist[YRT_SHADE_BINS + 1];
-  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x) hist[k] = 0;
-  qmap_load(qm, counts, YRT_QSEGS);  // barrier inside
-  unsigned lo, hi;
-  order_chunk(qm.pre[YRT_QSEGS], lo, hi);
-  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const int q = qmap_phys(qm, segCap, i);
-    const int tri = __float_as_int(hit[q].w);
-    const int key = tri < 0 ? YRT_SHADE_BINS : min(YRT_SHADE_BINS - 1, (int)((float)tri * binScale));
-    keys[i] = (uint16_t)key;
-    atomicAdd(&hist[key], 1u);
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x)
-    if (hist[k]) atomicAdd(binCount + k, hist[k]);
-}
-// one block: binCursor = exclusive prefix of binCount, binCount cleared for the next depth
-__global__ __launch_bounds__(1024) void k_order_scan(unsigned* __restrict__ binCount, unsigned* __restrict__ binCursor) {
-  constexpr int kPer = (YRT_SHADE_BINS + 1 + 1023) / 1024;
-  __shared__ unsigned waveSum[16];
-  const int t = threadIdx.x;
-  unsigned c[kPer], sum = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = t * kPer + j;
-    c[j] = k <= YRT_SHADE_BINS ? binCount[k] : 0u;
-    sum += c[j];
-  }
-  // inclusive scan of the per-thread sums: within the wave, then over the waves
-  unsigned inc = sum;
-  const int lane = t & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) waveSum[t >> 6] = inc;
-  __syncthreads();
-  unsigned waveBase = 0;
-  for (int w = 0; w < (t >> 6); ++w) waveBase += waveSum[w];
-  unsigned run = waveBase + inc - sum;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int k = t * kPer + j;
-    if (k <= YRT_SHADE_BINS) {
-      binCursor[k] = run;
-      binCount[k] = 0u;
-    }
-    run += c[j];
-  }
-}
-__global__ __launch_bounds__(YRT_ORDER_BLOCK) void k_order_scatter(const unsigned* __restrict__ counts, int segCap,
-                                                                   const uint16_t* __restrict__ keys,
-                                                                   unsigned* __restrict__ binCursor,
-                                                                   int* __restrict__ order) {
-  __shared__ QMap qm;
-  __shared__ unsigned pos[YRT_SHADE_BINS + 1];
-  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x) pos[k] = 0;
-  qmap_load(qm, counts, YRT_QSEGS);  // barrier inside
-  unsigned lo, hi;
-  order_chunk(qm.pre[YRT_QSEGS], lo, hi);
-  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&pos[keys[i]], 1u);
-  __syncthreads();
-  // this block's range of each bin
-  for (int k = threadIdx.x; k <= YRT_SHADE_BINS; k += blockDim.x)
-    if (pos[k]) pos[k] = atomicAdd(binCursor + k, pos[k]);
-  __syncthreads();
-  for (unsigned i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const unsigned at = atomicAdd(&pos[keys[i]], 1u);
-    order[at] = qmap_phys(qm, segCap, i);
-  }
-}
-void launch_shade_order(const PathBuffers& pb, int depth, int numTris, uint16_t* keys, unsigned* binWords, int* order,
-                        hipStream_t s) {
-  const unsigned* counts = pb.counters + qcounter_index(depth, 0, 0);
-  const float binScale = (float)YRT_SHADE_BINS / (float)(numTris > 0 ? numTris : 1);
-  unsigned* binCount = binWords;
-  unsigned* binCursor = binWords + YRT_SHADE_BINS + 1;
-  hipLaunchKernelGGL(k_order_count, dim3(YRT_ORDER_GRID), dim3(YRT_ORDER_BLOCK), 0, s, counts, pb.segCap, pb.hit,
-                     binScale, keys, binCount);
-  hipLaunchKernelGGL(k_order_scan, dim3(1), dim3(1024), 0, s, binCount, binCursor);
-  hipLaunchKernelGGL(k_order_scatter, dim3(YRT_ORDER_GRID), dim3(YRT_ORDER_BLOCK), 0, s, counts, pb.segCap, keys,
-                     binCursor, order);
 }
 
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s) {

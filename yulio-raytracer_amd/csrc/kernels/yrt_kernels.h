@@ -112,12 +112,6 @@ struct PathBuffers {
   // so the sum is deterministic and in the reference's order; k_shadow_resolve is not
   // launched. 0: sOcc + shFirst + k_shadow_resolve (several lights, light order kept).
   int fuseShadow;
-  // k_shade visits the queue through this permutation of its live slots when set
-  // (launch_shade_order: slots grouped by hit triangle), else in queue order
-  const int* shadeOrder = nullptr;
-  // 1: the depth-0 rays are stored at their path id (a fused depth 0, PrimaryRays), not at
-  // their queue slot: k_shade reads them through qPath
-  int rayByPath = 0;
 };
 
 // Fused shadow resolve: sContrib.w = path id (bits) whose pathL receives the contribution.
@@ -137,10 +131,9 @@ struct BatchInfo {
 // Camera rays generated inside the closest-hit kernel (k_trace<false, false, PRIM>):
 // depth 0 without a raygen pass. A lane takes the batch's next path id, computes its camera ray
 // as k_raygen does, traces it and, when it is done, either appends it with its hit to the
-// depth-0 queue (qPath/hit, the segment of its path id's 64-group; the ray itself is stored at
-// its path id in qOrg/qDir when generated, PathBuffers::rayByPath) or, on a miss, keeps the
-// radiance k_fill_paths gave every path before: the environment's (missL; direction-independent
-// environment lights only, k_shade's depth-0 miss branch). Paths outside the image get 0.
+// depth-0 queue (qPath/qOrg/qDir/hit, the segment of its path id's 64-group) or, on a miss,
+// writes the path's radiance: the environment's (GpuRenderParams::missL; direction-independent environment
+// lights only, k_shade's depth-0 miss branch). Paths outside the image get radiance 0.
 struct PrimaryRays {
   FrameView fv;
   BatchInfo bi;
@@ -150,7 +143,6 @@ struct PrimaryRays {
   float4* pathL;
   unsigned* counts;   // depth-0 closest-queue counters: qcounter_index(0, 0, 0), segments YRT_QCSTRIDE apart
   int segCap;
-  float4 missL;       // radiance of a depth-0 miss
   unsigned* traced;   // camera rays traced (valid paths); one atomic per wave
   long long numPaths; // numPixels * spp (grid size)
   int pinholeOnly;    // every frame's camera is a pinhole (a smaller instantiation)
@@ -183,21 +175,6 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
 void launch_shade(const SceneView& sv, const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, int depth,
                   unsigned materialMask, hipStream_t s);
 void launch_shadow_resolve(const PathBuffers& pb, int depth, int numLights, hipStream_t s);
-// Shading order of the closest queue entering `depth` (depth >= YRT_SHADE_ORDER_DEPTH): its
-// live slots grouped into YRT_SHADE_BINS ranges of the hit triangle id, misses last, so a
-// k_shade wave takes one material and neighbouring shading records, and the rays it emits
-// (continuations, shadow rays) leave in that order. A counting sort over the device-side count:
-// per-block LDS histograms (k_order_count), one scan (k_order_scan), a scatter of the slots
-// (k_order_scatter). binWords: 2 * (YRT_SHADE_BINS + 1) words, the first half zero on entry
-// (the scan clears it again); keys: capacity 16-bit words; order: capacity ints.
-#ifndef YRT_SHADE_BINS
-#define YRT_SHADE_BINS 2048
-#endif
-#ifndef YRT_SHADE_ORDER_DEPTH
-#define YRT_SHADE_ORDER_DEPTH 1
-#endif
-void launch_shade_order(const PathBuffers& pb, int depth, int numTris, uint16_t* keys, unsigned* binWords, int* order,
-                        hipStream_t s);
 void launch_resolve_pixels(const FrameView& fv, const PathBuffers& pb, const BatchInfo& bi, float* fbFloat,
                            uint8_t* fbRGB8, int rgb8Stride, float4* accu, int accumulate, hipStream_t s);
 // YRT_PROFILE builds only: SIMD-utilization counters of k_trace (see pathtrace.hip); -1 otherwise
