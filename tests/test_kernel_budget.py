@@ -1,0 +1,50 @@
+"""Register / scratch budgets of the built gfx950 kernels (CPU only: the code object's metadata,
+tools/code_object_resources.py). The traversal kernels' occupancy is part of their design
+(DESIGN §3, §8.5): a 64-lane block holds an 8 KB LDS stack ring, which allows 5 waves/SIMD, so
+a kernel above 96 VGPRs (or one that spills in its step loop) silently loses a wave per SIMD."""
+from pathlib import Path
+import shutil
+import sys
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tools"))
+
+from code_object_resources import DEFAULT_LIB, LLVM, kernel_resources  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not DEFAULT_LIB.exists() or not (LLVM / "clang-offload-bundler").exists()
+                                or shutil.which("c++filt") is None,
+                                reason="device library not built or ROCm LLVM tools absent")
+
+
+@pytest.fixture(scope="module")
+def res():
+    return kernel_resources(DEFAULT_LIB)
+
+
+def test_trace_kernels_fit_five_waves(res):
+    trace = {k: v for k, v in res.items() if "k_trace<" in k}
+    assert len(trace) == 8, sorted(trace)
+    for name, r in trace.items():
+        assert r["vgpr"] <= 96, (name, r)  # 512 / 5 waves, 8-register granularity
+        assert r["lds"] <= 8324, (name, r)
+    # no scratch in the queued trace kernels and in C4's fused depth 0 (any camera, compacted);
+    # the pinhole / identity fused instantiations reload a few camera-block values per refill
+    for name in ("k_trace<false, false, 0>", "k_trace<false, true, 0>", "k_trace<true, false, 0>",
+                 "k_trace<true, true, 0>", "k_trace<false, false, 2>"):
+        r = next(v for k, v in trace.items() if name in k)
+        assert r["scratch"] == 0, (name, r)
+    for name in ("k_trace<false, false, 1>", "k_trace<false, false, 3>", "k_trace<false, false, 4>"):
+        r = next(v for k, v in trace.items() if name in k)
+        assert r["scratch"] <= 32, (name, r)
+
+
+def test_shade_kernels_hold_four_waves(res):
+    shade = {k: v for k, v in res.items() if "k_shade<" in k}
+    assert shade
+    for name, r in shade.items():
+        if "8339454" in name:  # the generic every-material instantiation (2 waves, rare scenes)
+            continue
+        assert r["vgpr"] <= 128, (name, r)
+        assert r["scratch"] <= 16, (name, r)
