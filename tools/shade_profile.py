@@ -40,6 +40,8 @@ if rc != 0:
     sys.exit("not a YRT_SHADE_PROF build")
 tot = sum(v)
 items = st["raysClosest"]
+if tot == 0:
+    sys.exit(f"{cfg}: no phase cycles recorded (the profile counters stayed 0)")
 print(f"{cfg} {size}^2 {spp}spp: shade items {items:.0f}, shade ms {st['msShade']:.1f}")
 for name, x in zip(PHASES, v):
     print(f"  {name:38s} {100.0 * x / tot:6.2f} %   {x / max(items, 1) * 64:9.1f} wave-cycles per 64 items")
