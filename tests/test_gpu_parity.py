@@ -335,11 +335,11 @@ def test_batch_capacity_invariance(gpu_device):
 @pytest.mark.parametrize("which", ["C3", "C4"])
 def test_fused_primary_invariance(gpu_device, monkeypatch, which):
     """Depth 0 as one kernel (camera rays generated inside the closest-hit trace,
-    launch_trace_primary) — hits compacted and misses resolved there (YRT_PRIMARY=2), or every
-    path in its own slot (identity layout, 3) — against k_raygen + the queued trace (0):
-    bit-identical frames and the same query counts; C3's dome and C4's zero HDRI both qualify."""
+    launch_trace_primary: hits queued, misses resolved there; YRT_PRIMARY=2) against k_raygen +
+    the queued trace (0): bit-identical frames and the same query counts; C3's dome and C4's
+    zero HDRI both qualify (C3: pinhole camera, C4: stereo)."""
     out = []
-    for prim in ("0", "2", "3"):
+    for prim in ("0", "2"):
         monkeypatch.setenv("YRT_PRIMARY", prim)
         gpu_device.set_batch_capacity(256 * 16 * 5)  # several batches on both lanes
         try:

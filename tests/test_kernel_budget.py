@@ -25,19 +25,13 @@ def res():
 
 def test_trace_kernels_fit_five_waves(res):
     trace = {k: v for k, v in res.items() if "k_trace<" in k}
-    assert len(trace) == 8, sorted(trace)
+    # closest hit (static, moving), the fused depth 0, any hit (static, moving)
+    assert len(trace) == 5, sorted(trace)
     for name, r in trace.items():
         assert r["vgpr"] <= 96, (name, r)  # 512 / 5 waves, 8-register granularity
         assert r["lds"] <= 8324, (name, r)
-    # no scratch in the queued trace kernels and in C4's fused depth 0 (any camera, compacted);
-    # the pinhole / identity fused instantiations reload a few camera-block values per refill
-    for name in ("k_trace<false, false, 0>", "k_trace<false, true, 0>", "k_trace<true, false, 0>",
-                 "k_trace<true, true, 0>", "k_trace<false, false, 2>"):
-        r = next(v for k, v in trace.items() if name in k)
         assert r["scratch"] == 0, (name, r)
-    for name in ("k_trace<false, false, 1>", "k_trace<false, false, 3>", "k_trace<false, false, 4>"):
-        r = next(v for k, v in trace.items() if name in k)
-        assert r["scratch"] <= 32, (name, r)
+    assert any("k_trace<false, false, 1>" in k for k in trace)
 
 
 def test_shade_kernels_hold_four_waves(res):

@@ -67,8 +67,7 @@ struct GpuCtx {
       hipEvent_t done = nullptr;
       int64_t tiles = 0;
       int64_t seq = 0;
-      bool fused = false;  // depth 0 ran as k_trace's camera-ray instantiation
-      bool compact = false;  // ... with its hits compacted (the depth-0 queue count = its hits)
+      bool fused = false;  // depth 0 ran as k_trace's camera-ray instantiation (hits queued only)
     };
     static constexpr int kPendDepth = 1;
     Pend pend[kPendDepth];
@@ -787,10 +786,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           nc += Pd.hc[qcounter_index(d, 0, k)];
           ns += Pd.hc[qcounter_index(d, 1, k)];
         }
-        if (d == 0 && Pd.fused && Pd.compact && Pd.hc[tracedWord] > 0) {
+        if (d == 0 && Pd.fused && Pd.hc[tracedWord] > 0) {
           if (g.missFrac.size() > 64 && !g.missFrac.count(G.serial)) g.missFrac.clear();
           auto& acc = g.missFrac[G.serial];
-          acc.first += (double)Pd.hc[tracedWord] - nc;  // a compact depth 0 queues its hits only
+          acc.first += (double)Pd.hc[tracedWord] - nc;  // a fused depth 0 queues its hits only
           acc.second += (double)Pd.hc[tracedWord];
           missEst = acc.first / acc.second;
         }
@@ -818,17 +817,15 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // depth-0 miss radiance is a constant: no backplate, every environment light ambient
     // (k_shade's miss branch then adds thr * L = L per light in envLights order, thr = 1).
     // Not in the capture frame (it copies the depth-0 queue). It pays where camera rays miss
-    // (C4: cube job -11 %) and costs where they hit (C3 -2.5 %, C5 -1.3 %: the kernel runs at 4
-    // waves/SIMD and its hits are appended scattered, profiles/r04/ab_r04d.txt), so a batch is
-    // fused while the scene's measured miss share (missFrac, over its fused batches so far) is at
-    // least YRT_PRIMARY_MISS (default 0.5) or unknown. YRT_PRIMARY=0: never, 2: always.
+    // (C4: cube job -11 %, -1.3 % more at 96 VGPRs / 5 waves since round 5) and costs where they
+    // hit (C3 -2.5 %, C5 -1.3 %: its hits are appended in completion order, profiles/r04/
+    // ab_r04d.txt; a path-ordered "identity" layout measured no better, profiles/r05/
+    // ab_prim_r05j.txt), so a batch is fused while the scene's measured miss share (missFrac, over
+    // its fused batches so far) is at least YRT_PRIMARY_MISS (default 0.5) or unknown.
+    // YRT_PRIMARY=0: never, 2: always.
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
-    const bool primIdentity = getenv("YRT_PRIMARY_IDENTITY") && atoi(getenv("YRT_PRIMARY_IDENTITY")) != 0;
-    const bool identityOk = rp.maxDepth > 0 && !(1.0f < rp.minContribution);
-    bool allPinhole = true;
-    for (int k = 0; k < nf; ++k) allPinhole &= g.hCams[k].type == CAM_PINHOLE;
     for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
       const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - first);
       if (R.stopFlag && R.stopFlag->load()) break;
@@ -863,11 +860,9 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bi.tileOffset = index;
       bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
       HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
-      // compact (hits queued) while camera rays mostly miss; identity layout (YRT_PRIMARY=3, or
-      // YRT_PRIMARY_IDENTITY=1 for the scenes whose rays mostly hit) or k_raygen otherwise
-      const bool compactBatch = primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss));
-      const bool identityBatch = !compactBatch && identityOk && (primMode == 3 || (primMode == 1 && primIdentity));
-      const bool fusedBatch = fusedPrimary && (compactBatch || identityBatch);
+      // fused (hits queued) while camera rays mostly miss, k_raygen + the queued trace otherwise
+      const bool fusedBatch =
+          fusedPrimary && (primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss)));
       if (!fusedBatch) launch_raygen(fv, pb, bi, st);
       for (int d = 0; d < rp.maxDepth; ++d) {
         const int cur = d & 1;
@@ -885,8 +880,6 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           pr.segCap = pb.segCap;
           pr.traced = pb.counters + tracedWord;
           pr.numPaths = (long long)bi.numPixels * spp;
-          pr.pinholeOnly = allPinhole ? 1 : 0;
-          pr.identity = compactBatch ? 0 : 1;
           launch_trace_primary(lsv, pr, pb.hit, st);
         } else {
           launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
@@ -920,7 +913,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       HIP_CHECK(hipEventRecord(Pd.done, st));
       Pd.tiles = bi.numPixels / 256;
       Pd.fused = fusedBatch;
-      Pd.compact = fusedBatch && compactBatch;
+
       Pd.seq = batch;
       L.pendCount += 1;
       launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,

@@ -465,10 +465,9 @@ __device__ __forceinline__ GpuTri tri_at(const GpuTri* __restrict__ tris, const 
 
 // MOTION: moving geometry; rayTime[q] is query q's time (Ray::time, set from sample.getTime()
 // for camera rays and inherited by shadow and continuation rays, pathtraceintegrator.cpp:158,210)
-// PRIM (closest hit, static scenes): depth 0 from the batch's path ids instead of a queue —
+// PRIM = 1 (closest hit, static scenes): depth 0 from the batch's path ids instead of a queue —
 // camera rays generated at refill, hits appended to the depth-0 queue, misses resolved
-// (PrimaryRays); 1 / 3: pinhole cameras only (the other cameras' code would cost registers),
-// 2 / 4: any camera; 3 / 4: identity layout (PrimaryRays::identity), 1 / 2: hits compacted
+// (PrimaryRays)
 template <bool ANY, bool MOTION, int PRIM = 0>
 __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(
     ANY ? YRT_TRACE_WAVES_ANY : PRIM ? YRT_TRACE_WAVES_PRIM : YRT_TRACE_WAVES))) void k_trace(
@@ -480,18 +479,12 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          ShadowFuse sf, const float* __restrict__ rayTime,
                                                          PrimaryRays pr) {
   static_assert(!PRIM || (!ANY && !MOTION), "camera rays: closest hit, static scenes");
-  constexpr bool kPinhole = PRIM == 1 || PRIM == 3, kIdentity = PRIM >= 3;
   constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
   __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   unsigned n;
   if constexpr (PRIM) {
     n = (unsigned)pr.bi.numPixels * (unsigned)const_ref(pr.fv.rp).spp;
-    // identity layout: the depth-0 queue's segments are full up to n (logical slot = path id)
-    if (kIdentity && blockIdx.x == 0 && threadIdx.x < YRT_QSEGS) {
-      const long long c = (long long)n - (long long)threadIdx.x * pr.segCap;
-      pr.counts[(size_t)threadIdx.x * YRT_QCSTRIDE] = (unsigned)(c < 0 ? 0 : c > pr.segCap ? pr.segCap : c);
-    }
   } else {
     qmap_load(qm, counts, numSegs);
     n = qm.pre[YRT_QSEGS];
@@ -564,19 +557,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // them). The camera rays traced are counted after the loop, no counter is carried through it.
   auto prim_store = [&]() {
     const bool hitp = best.tri >= 0;
-    if constexpr (!kIdentity) {
-      if (!hitp) {
-        const float* mL = pr.fv.rp->missL;
-        pr.pathL[q] = make_float4(mL[0], mL[1], mL[2], mL[3]);
-      }
-    }
-    if constexpr (kIdentity) {
-      // identity layout: every path keeps its own slot, misses included (k_shade shades them)
-      pr.qPath[q] = q;
-      pr.qOrg[q] = ro;
-      pr.qDir[q] = rd;
-      hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
-      return;
+    if (!hitp) {
+      const float* mL = pr.fv.rp->missL;
+      pr.pathL[q] = make_float4(mL[0], mL[1], mL[2], mL[3]);
     }
     const int seg = qseg_of((unsigned)q);
     unsigned long long m = ballot(hitp);
@@ -637,7 +620,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                 const int rec = pr.fv.pixelSets[(size_t)y * rp.width + x] * rp.spp + smp;
                 const float fx = (float(x) + samp(pr.fv, 0, rec)) * rp.rcpWidth;
                 const float fy = (float(y) + samp(pr.fv, 1, rec)) * rp.rcpHeight;
-                const float lx = kPinhole ? 0.f : samp(pr.fv, 2, rec), ly = kPinhole ? 0.f : samp(pr.fv, 3, rec);
+                const float lx = samp(pr.fv, 2, rec), ly = samp(pr.fv, 3, rec);
                 V3 o3 = v3s(0.f), d3 = v3s(0.f);
                 // one pass per frame among the refilled lanes (almost always one): the frame's
                 // camera record is read with scalar loads, as in k_raygen
@@ -645,10 +628,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                   const int f0 = __builtin_amdgcn_readfirstlane(f);
                   if (f == f0) {
                     const YRT_CONST GpuCamera& cam = const_ref(pr.fv.cam + f0);
-                    if constexpr (kPinhole)
-                      pinhole_ray(cam, fx, fy, o3, d3);
-                    else
-                      camera_ray(cam, fx, fy, o3, d3, lx, ly);
+                    camera_ray(cam, fx, fy, o3, d3, lx, ly);
                     todo = false;
                   }
                 }
@@ -660,11 +640,6 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                 // four registers (spilled at a 5-wave register target)
                 const float z = opaque_zero();
                 pr.pathL[p] = make_float4(z, z, z, z);  // not a pixel of the image
-                if constexpr (kIdentity) {
-                  // its slot reads as a miss (k_shade's miss adds go to a pixel no resolve reads)
-                  pr.qPath[p] = p;
-                  hitOut[p] = make_float4(z, z, z, __int_as_float(-1));
-                }
                 q = -1;
                 ro = make_float4(0.f, 0.f, 0.f, 1.f);  // tfar < tnear: nothing to traverse
                 rd = make_float4(0.f, 0.f, 1.f, 0.f);
@@ -1866,18 +1841,9 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
 
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
-#define YRT_LAUNCH_PRIM(k)                                                                                 \
-  hipLaunchKernelGGL((k_trace<false, false, k>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr, \
-                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,      \
-                     ShadowFuse{}, (const float*)nullptr, pr)
-  if (pr.identity) {
-    if (pr.pinholeOnly) YRT_LAUNCH_PRIM(3);
-    else YRT_LAUNCH_PRIM(4);
-  } else {
-    if (pr.pinholeOnly) YRT_LAUNCH_PRIM(1);
-    else YRT_LAUNCH_PRIM(2);
-  }
-#undef YRT_LAUNCH_PRIM
+  hipLaunchKernelGGL((k_trace<false, false, 1>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
+                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
+                     ShadowFuse{}, (const float*)nullptr, pr);
 }
 
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,

@@ -145,12 +145,6 @@ struct PrimaryRays {
   int segCap;
   unsigned* traced;   // camera rays traced (valid paths); one atomic per wave
   long long numPaths; // numPixels * spp (grid size)
-  int pinholeOnly;    // every frame's camera is a pinhole (a smaller instantiation)
-  // 1: identity layout — every path id p keeps queue slot p (misses and paths outside the image
-  // included, the depth-0 segment counts written full): the queue in path order, k_shade shades
-  // the misses as after k_raygen (for scenes whose camera rays mostly hit; needs maxDepth > 0
-  // and minContribution <= 1, so that every pixel's path is queued)
-  int identity;
 };
 
 // Kernel launchers (kernels/pathtrace.hip)
