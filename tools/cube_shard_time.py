@@ -10,6 +10,8 @@ is the slowest share; efficiency = T(1) / (N * T(N)).
       renderer.cpp:742-878)
   C5: the Frederick stand-in (yrt.frederick) FPR view, 12 x 1536^2 at 1024 spp (renderer.cpp:
       543-737: faceCamera update, scene commit, render)
+  C3: the bench frame (Sponza stand-in 2048^2 at 64 spp): one rank's share of one frame, as
+      bench.py's weak-scaling step renders it N times per step (--mode is ignored)
 
 --mode face: one rtRenderFrame per face (the reference's loop);
 --mode cube: the 12 faces in one yrtRenderFrames call (tiles of all faces in one sequence).
@@ -35,6 +37,9 @@ import yrt  # noqa: E402
 
 
 def session(cfg, dev, size, spp):
+    if cfg == "C3":
+        from helpers import c3_args
+        return yrt.Session(c3_args(size, spp), device=dev)
     if cfg == "C4":
         from helpers import c4_args
         return yrt.Session(c4_args(size, spp), device=dev)
@@ -48,6 +53,10 @@ def session(cfg, dev, size, spp):
 def render_cube(ses, cfg, mode):
     """One full cubemap; returns rays traced (closest + shadow)."""
     dev = ses.device
+    if cfg == "C3":  # one frame (bench.py's step at N = 1; at N GPUs each rank renders its share)
+        ses.render(read=False)
+        st = dev.render_stats()
+        return st["raysClosest"] + st["raysShadow"]
     # render only: the frames are written back into the session's (host) framebuffers as the
     # product does, but not converted to numpy here
     if mode == "cube":
@@ -70,7 +79,7 @@ def render_cube(ses, cfg, mode):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("cfg", choices=["C4", "C5"])
+    ap.add_argument("cfg", choices=["C3", "C4", "C5"])
     ap.add_argument("--mode", choices=["face", "cube"], default="face")
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to time")
@@ -79,7 +88,9 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
     a = ap.parse_args()
-    spp = a.spp or (256 if a.cfg == "C4" else 1024)
+    spp = a.spp or {"C3": 64, "C4": 256, "C5": 1024}[a.cfg]
+    if a.cfg == "C3" and a.size == 1536:
+        a.size = 2048
     dev = yrt.Device(0)
     if a.capacity:
         dev.set_batch_capacity(a.capacity)
