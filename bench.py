@@ -196,7 +196,7 @@ def main():
         dev.set_lanes(1)
         dev.rtRenderFrame(R, cam, S, T, F, 0)
         serial = dev.render_stats()
-        dev.set_lanes(int(os.environ.get("YRT_LANES", "2")))
+        dev.set_lanes(0)  # back to the default (4, or YRT_LANES)
 
     stereo = stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used) if a.stereo_frames > 0 else None
 

@@ -173,9 +173,9 @@ typedef struct YRTRenderStats {
 YRT_API int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out);
 /* 1 = bracket every kernel with HIP events (adds sync-free event records). */
 YRT_API int yrtSetKernelTiming(YRTDevice dev, int enable);
-/* Wavefront lanes (HIP streams whose batches overlap) of every render context, 1..4 (default 2,
- * or YRT_LANES). With one lane no two kernels of a frame overlap, so the kernel timings above
- * are each kernel's own duration (bench.py's roofline uses such a frame). */
+/* Wavefront lanes (HIP streams whose batches overlap) of every render context, 1..4; 0 = the
+ * default (4, or YRT_LANES). With one lane no two kernels of a frame overlap, so the kernel
+ * timings above are each kernel's own duration (bench.py's roofline uses such a frame). */
 YRT_API int yrtSetLanes(YRTDevice dev, int lanes);
 /* Scene info: triangles, geometries, BVH nodes, BVH depth, build seconds; numTriRefs = leaf
  * triangle records (>= numTriangles: spatial splits reference a triangle from several leaves). */

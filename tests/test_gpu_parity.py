@@ -361,17 +361,22 @@ def test_fused_primary_invariance(gpu_device, monkeypatch, which):
 
 
 def test_lanes_invariance(monkeypatch):
-    """Batches spread over one or two lanes (streams) give bit-identical frames."""
+    """Batches spread over one, two or four lanes (streams) give bit-identical frames; lanes 0
+    restores the default."""
     imgs = []
-    for lanes in ("1", "2"):
+    for lanes in ("1", "2", "4"):
         monkeypatch.setenv("YRT_LANES", lanes)
         d = yrt.Device(0)
         d.set_batch_capacity(256 * 4 * 5)
         s = _session(d, c2_args(160, 4))
         imgs.append(s.render())
+        if lanes == "1":
+            d.set_lanes(0)  # the default again (YRT_LANES = 1 here)
+            assert np.array_equal(s.render(), imgs[-1])
         s.close()
         d.close()
     assert np.array_equal(imgs[0], imgs[1])
+    assert np.array_equal(imgs[0], imgs[2])
 
 
 def test_rgb8_framebuffer_quantization(gpu_device):

@@ -74,7 +74,14 @@ struct GpuCtx {
     int pendHead = 0, pendCount = 0;
   };
   static constexpr int kMaxLanes = 4;      // YRT_LANES may ask for up to 4 (the sweeps of DESIGN §3)
-  static constexpr int kDefaultLanes = 2;  // two: C3 +4 % over one, three or four no better
+  // four: C3 +1.4 %, C4 cube job -2 % (N = 8 share -1.5 %), C5 -0.5 % over two on the same box
+  // (profiles/r05/ab_lanes_r05q.txt); in rounds 1-2 two were +4 % over one, and more no better
+  static constexpr int kDefaultLanes = 4;
+  static int default_lanes() {
+    int lanes = kDefaultLanes;
+    if (const char* e = getenv("YRT_LANES")) lanes = std::max(1, std::min(kMaxLanes, atoi(e)));
+    return lanes;
+  }
   Lane lanes[kMaxLanes];
   int numLanes = kDefaultLanes;
   DevBuf dRp, dCam, dPixelSets, dAccu, dCount, dSpill, dSlab, dDirect;
@@ -242,8 +249,7 @@ class Device {
   bool gpu = true;  // false: host-only device (loaders, BVH, export; no rendering) for CPU tests
   Device(const std::vector<int>& devs, bool useGpu) : gpu(useGpu) {
     if (!gpu) return;
-    int lanes = GpuCtx::kDefaultLanes;
-    if (const char* e = getenv("YRT_LANES")) lanes = std::max(1, std::min(GpuCtx::kMaxLanes, atoi(e)));
+    const int lanes = GpuCtx::default_lanes();
     for (int d : devs) ctx.emplace_back(new GpuCtx(d, lanes));
     hipDevice = ctx[0]->hipDevice;
     stream = ctx[0]->stream;
@@ -1802,8 +1808,8 @@ int yrtSetKernelTiming(YRTDevice dev, int enable) {
 }
 int yrtSetLanes(YRTDevice dev, int lanes) {
   DEV_GUARD(dev, -1)
-  if (lanes < 1 || lanes > GpuCtx::kMaxLanes) throw std::runtime_error("yrtSetLanes: 1..4 lanes");
-  for (auto& c : dev->d->ctx) c->numLanes = lanes;
+  if (lanes < 0 || lanes > GpuCtx::kMaxLanes) throw std::runtime_error("yrtSetLanes: 1..4 lanes, 0 = default");
+  for (auto& c : dev->d->ctx) c->numLanes = lanes ? lanes : GpuCtx::default_lanes();
   return 0;
   DEV_END(-1)
 }

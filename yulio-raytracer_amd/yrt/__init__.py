@@ -304,7 +304,8 @@ class Device:
         self._rc(N.dev.yrtSetKernelTiming(self.h, int(on)), "set_kernel_timing")
 
     def set_lanes(self, lanes):
-        """Wavefront lanes (overlapping HIP streams), 1..4; with 1 no two kernels overlap."""
+        """Wavefront lanes (overlapping HIP streams), 1..4 (0: the default, 4 or YRT_LANES); with 1
+        no two kernels overlap."""
         self._rc(N.dev.yrtSetLanes(self.h, int(lanes)), "set_lanes")
 
     def scene_info(self, scene) -> dict:
