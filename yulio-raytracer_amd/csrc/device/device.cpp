@@ -73,7 +73,10 @@ struct GpuCtx {
     Pend pend[kPendDepth];
     int pendHead = 0, pendCount = 0;
   };
-  static constexpr int kMaxLanes = 4;      // YRT_LANES may ask for up to 4 (the sweeps of DESIGN §3)
+#ifndef YRT_MAX_LANES
+#define YRT_MAX_LANES 4  // one HIP stream each; HIP gives a process 4 hardware queues by default
+#endif
+  static constexpr int kMaxLanes = YRT_MAX_LANES;  // YRT_LANES may ask for up to this many
   // four: C3 +1.4 %, C4 cube job -2 % (N = 8 share -1.5 %), C5 -0.5 % over two on the same box
   // (profiles/r05/ab_lanes_r05q.txt); in rounds 1-2 two were +4 % over one, and more no better
   static constexpr int kDefaultLanes = 4;
