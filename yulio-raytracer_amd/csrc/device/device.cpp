@@ -29,6 +29,9 @@
 
 namespace yrt {
 
+#ifndef YRT_BATCH_INTERLEAVE
+#define YRT_BATCH_INTERLEAVE 1
+#endif
 #ifndef YRT_STACK_DEPTH
 #define YRT_STACK_DEPTH 64
 #endif
@@ -835,49 +838,41 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
     const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
-    for (int64_t first = 0; first < shardTiles; first += tilesPerBatch, ++batch) {
-      const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - first);
-      if (R.stopFlag && R.stopFlag->load()) break;
-      // the batch goes to the first lane with room in its ring: finished batches are accounted
-      // as they arrive, on any lane, so a lane that finishes early is refilled at once instead
-      // of waiting for the other lane's older batch (lanes in turn: C4 N = 3 rank share 160 ms,
-      // profiles/r04/ab_r04i.txt). When every ring is full the host blocks on the batch enqueued
-      // first (hipEventSynchronize) instead of spinning a core.
-      int li = -1;
-      for (;;) {
-        for (int l = 0; l < nl; ++l)
-          while (drain_one(g.lanes[l], false)) {}
-        for (int l = 0; l < nl; ++l)
-          if (g.lanes[l].pendCount < GpuCtx::Lane::kPendDepth &&
-              (li < 0 || g.lanes[l].pendCount < g.lanes[li].pendCount))
-            li = l;
-        if (li >= 0) break;
-        int oldest = 0;
-        for (int l = 1; l < nl; ++l)
-          if (g.lanes[l].pend[g.lanes[l].pendHead].seq < g.lanes[oldest].pend[g.lanes[oldest].pendHead].seq) oldest = l;
-        drain_one(g.lanes[oldest], true);
-      }
-      GpuCtx::Lane& L = g.lanes[li];
+    // A lane's batch is enqueued a step at a time — its prologue (counter clear, camera rays),
+    // one depth (closest trace, shade, shadow trace), its epilogue (counter copy, pixel resolve)
+    // — round-robin over the lanes that hold a batch, so every lane's first kernels are queued
+    // within a few launches of the job's start. A whole batch at a time (≈ 33 launches at
+    // ≈ 58 µs of host time each), lane k started k × 1.9 ms after lane 0 and the job's end waited
+    // as long for the last lane (C3 N = 8 share: lanes starting 0 / 1.1 / 3.1 / 5.1 ms into a
+    // 52.7 ms job, profiles/r05/timeline_c3_n8_r05v.txt). A lane takes its next batch once its
+    // previous batch's counters have arrived (Pend); the batch goes to the first such lane, so a
+    // lane that finishes early is refilled at once (lanes in turn: C4 N = 3 rank share 160 ms,
+    // profiles/r04/ab_r04i.txt). When every lane is full the host blocks on the batch enqueued
+    // first (hipEventSynchronize) instead of spinning a core.
+    struct LaneJob {
+      bool active = false;
+      int step = 0;  // 0: prologue, 1..maxDepth: depth step - 1, maxDepth + 1: epilogue
+      int64_t first = 0, seq = 0;
+      BatchInfo bi{};
+      bool fused = false;
+    };
+    std::vector<LaneJob> jobs(nl);
+    int64_t nextFirst = 0, nextBatch = 0;  // contiguous: the next batch's first tile; interleaved: its index
+    auto enqueue_step = [&](GpuCtx::Lane& L, LaneJob& J) {
       const hipStream_t st = L.stream;
       const PathBuffers pb = lane_buffers(L);
       SceneView lsv = sv;
       lsv.traceSpill = L.spill.as<int>();
-      BatchInfo bi;
-      bi.firstTile = (int)first;
-      bi.numPixels = (int)(batchTiles * 256);
-      bi.tileStride = count;
-      bi.tileOffset = index;
-      bi.divPixels = fastdiv_make((uint32_t)bi.numPixels);
-      HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
-      // fused (hits queued) while camera rays mostly miss, k_raygen + the queued trace otherwise
-      const bool fusedBatch =
-          fusedPrimary && (primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss)));
-      if (!fusedBatch) launch_raygen(fv, pb, bi, st);
-      for (int d = 0; d < rp.maxDepth; ++d) {
+      const BatchInfo& bi = J.bi;
+      if (J.step == 0) {
+        HIP_CHECK(hipMemsetAsync(L.counters.p, 0, counterWords * sizeof(unsigned), st));
+        if (!J.fused) launch_raygen(fv, pb, bi, st);
+      } else if (J.step <= rp.maxDepth) {
+        const int d = J.step - 1;
         const int cur = d & 1;
         EvPair e1{};
         if (kernelTiming) { e1 = {g.ev(), g.ev(), 0}; HIP_CHECK(hipEventRecord(e1.a, st)); }
-        if (d == 0 && fusedBatch) {
+        if (d == 0 && J.fused) {
           PrimaryRays pr;
           pr.fv = fv;
           pr.bi = bi;
@@ -895,7 +890,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
                                pb.segCap, pb.hit, st, pb.qTime[cur]);
         }
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
-        if (captureMax > 0 && first == 0)
+        if (captureMax > 0 && J.first == 0)
           g.capture(captureMax, g.capClosest, d, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0),
                     pb.segCap, st);
         EvPair e2{};
@@ -909,24 +904,75 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           launch_trace_any(lsv, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0), YRT_QSEGS, pb.shSegCap,
                            pb.sOcc, st, &sf, pb.sTime);
           if (kernelTiming) { HIP_CHECK(hipEventRecord(e3.b, st)); evs.push_back(e3); }
-          if (captureMax > 0 && first == 0)
+          if (captureMax > 0 && J.first == 0)
             g.capture(captureMax, g.capShadow, d, pb.sOrg, pb.sDir, pb.counters + qcounter_index(d, 1, 0),
                       pb.shSegCap, st);
           if (!pb.fuseShadow) launch_shadow_resolve(pb, d, numDirect, st);
         }
+      } else {
+        // the counters are final after the last trace: their copy runs before the pixel resolve,
+        // so the host learns the batch's queue sizes while the resolve still runs
+        GpuCtx::Lane::Pend& Pd = L.pend[(L.pendHead + L.pendCount) % GpuCtx::Lane::kPendDepth];
+        HIP_CHECK(hipMemcpyAsync(Pd.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipEventRecord(Pd.done, st));
+        Pd.tiles = bi.numPixels / 256;
+        Pd.fused = J.fused;
+        Pd.seq = J.seq;
+        L.pendCount += 1;
+        launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride, g.dAccu.as<float4>(),
+                              accumulate ? 1 : 0, st);
+        J.active = false;
       }
-      // the counters are final after the last trace: their copy runs before the pixel resolve,
-      // so the host learns the batch's queue sizes while the resolve still runs
-      GpuCtx::Lane::Pend& Pd = L.pend[(L.pendHead + L.pendCount) % GpuCtx::Lane::kPendDepth];
-      HIP_CHECK(hipMemcpyAsync(Pd.hc, L.counters.p, counterWords * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipEventRecord(Pd.done, st));
-      Pd.tiles = bi.numPixels / 256;
-      Pd.fused = fusedBatch;
-
-      Pd.seq = batch;
-      L.pendCount += 1;
-      launch_resolve_pixels(fv, pb, bi, g.fbFloat(), g.fbRGB8(), (int)rgb8Stride,
-                            g.dAccu.as<float4>(), accumulate ? 1 : 0, st);
+      J.step += 1;
+    };
+    for (;;) {
+      if (R.stopFlag && R.stopFlag->load()) nextFirst = shardTiles, nextBatch = numBatches;  // no new batches
+      for (int l = 0; l < nl; ++l)
+        while (drain_one(g.lanes[l], false)) {}
+      for (int l = 0; l < nl && nextFirst < shardTiles && nextBatch < numBatches; ++l) {
+        LaneJob& J = jobs[l];
+        if (J.active || g.lanes[l].pendCount >= GpuCtx::Lane::kPendDepth) continue;
+        J = LaneJob{};
+        J.active = true;
+        J.seq = batch++;
+#if YRT_BATCH_INTERLEAVE
+        // batch b holds the shard's tiles j = b, b + numBatches, ...: every batch spans the whole
+        // image, so the lanes' batches cost alike (contiguous tile ranges are image bands of
+        // unequal cost: a C3 N = 8 share's last quarter of rows ran 10 % longer than the others)
+        const int64_t b = nextBatch++;
+        const int64_t batchTiles = (shardTiles - b + numBatches - 1) / numBatches;
+        J.first = b;
+        J.bi.firstTile = 0;
+        J.bi.tileStride = count * (int)numBatches;
+        J.bi.tileOffset = index + (int)b * count;
+        if (nextBatch >= numBatches) nextFirst = shardTiles;
+#else
+        const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - nextFirst);
+        J.first = nextFirst;
+        J.bi.firstTile = (int)nextFirst;
+        J.bi.tileStride = count;
+        J.bi.tileOffset = index;
+        nextFirst += batchTiles;
+        if (nextFirst >= shardTiles) nextBatch = numBatches;
+#endif
+        J.bi.numPixels = (int)(batchTiles * 256);
+        J.bi.divPixels = fastdiv_make((uint32_t)J.bi.numPixels);
+        // fused (hits queued) while camera rays mostly miss, k_raygen + the queued trace otherwise
+        J.fused = fusedPrimary && (primMode == 2 || (primMode == 1 && (missEst < 0 || missEst >= primMiss)));
+      }
+      bool enqueued = false;
+      for (int l = 0; l < nl; ++l)
+        if (jobs[l].active) {
+          enqueue_step(g.lanes[l], jobs[l]);
+          enqueued = true;
+        }
+      if (enqueued) continue;
+      if (nextFirst >= shardTiles || nextBatch >= numBatches) break;  // every batch enqueued
+      // every lane holds a batch whose counters have not arrived: wait for the oldest
+      int oldest = 0;
+      for (int l = 1; l < nl; ++l)
+        if (g.lanes[l].pend[g.lanes[l].pendHead].seq < g.lanes[oldest].pend[g.lanes[oldest].pendHead].seq) oldest = l;
+      drain_one(g.lanes[oldest], true);
     }
     for (int l = 0; l < nl; ++l)
       while (drain_one(g.lanes[l], true)) {}
