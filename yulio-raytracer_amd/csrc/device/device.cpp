@@ -29,9 +29,6 @@
 
 namespace yrt {
 
-#ifndef YRT_BATCH_INTERLEAVE
-#define YRT_BATCH_INTERLEAVE 1
-#endif
 #ifndef YRT_STACK_DEPTH
 #define YRT_STACK_DEPTH 64
 #endif
@@ -857,7 +854,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       bool fused = false;
     };
     std::vector<LaneJob> jobs(nl);
-    int64_t nextFirst = 0, nextBatch = 0;  // contiguous: the next batch's first tile; interleaved: its index
+    int64_t nextFirst = 0;  // the next batch's first tile of the shard
     auto enqueue_step = [&](GpuCtx::Lane& L, LaneJob& J) {
       const hipStream_t st = L.stream;
       const PathBuffers pb = lane_buffers(L);
@@ -926,35 +923,21 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
       J.step += 1;
     };
     for (;;) {
-      if (R.stopFlag && R.stopFlag->load()) nextFirst = shardTiles, nextBatch = numBatches;  // no new batches
+      if (R.stopFlag && R.stopFlag->load()) nextFirst = shardTiles;  // no new batches
       for (int l = 0; l < nl; ++l)
         while (drain_one(g.lanes[l], false)) {}
-      for (int l = 0; l < nl && nextFirst < shardTiles && nextBatch < numBatches; ++l) {
+      for (int l = 0; l < nl && nextFirst < shardTiles; ++l) {
         LaneJob& J = jobs[l];
         if (J.active || g.lanes[l].pendCount >= GpuCtx::Lane::kPendDepth) continue;
         J = LaneJob{};
         J.active = true;
         J.seq = batch++;
-#if YRT_BATCH_INTERLEAVE
-        // batch b holds the shard's tiles j = b, b + numBatches, ...: every batch spans the whole
-        // image, so the lanes' batches cost alike (contiguous tile ranges are image bands of
-        // unequal cost: a C3 N = 8 share's last quarter of rows ran 10 % longer than the others)
-        const int64_t b = nextBatch++;
-        const int64_t batchTiles = (shardTiles - b + numBatches - 1) / numBatches;
-        J.first = b;
-        J.bi.firstTile = 0;
-        J.bi.tileStride = count * (int)numBatches;
-        J.bi.tileOffset = index + (int)b * count;
-        if (nextBatch >= numBatches) nextFirst = shardTiles;
-#else
         const int64_t batchTiles = std::min<int64_t>(tilesPerBatch, shardTiles - nextFirst);
         J.first = nextFirst;
         J.bi.firstTile = (int)nextFirst;
         J.bi.tileStride = count;
         J.bi.tileOffset = index;
         nextFirst += batchTiles;
-        if (nextFirst >= shardTiles) nextBatch = numBatches;
-#endif
         J.bi.numPixels = (int)(batchTiles * 256);
         J.bi.divPixels = fastdiv_make((uint32_t)J.bi.numPixels);
         // fused (hits queued) while camera rays mostly miss, k_raygen + the queued trace otherwise
@@ -967,7 +950,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           enqueued = true;
         }
       if (enqueued) continue;
-      if (nextFirst >= shardTiles || nextBatch >= numBatches) break;  // every batch enqueued
+      if (nextFirst >= shardTiles) break;  // every batch enqueued
       // every lane holds a batch whose counters have not arrived: wait for the oldest
       int oldest = 0;
       for (int l = 1; l < nl; ++l)
