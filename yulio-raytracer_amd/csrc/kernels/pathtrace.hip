@@ -375,7 +375,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 // This keeps 64-wide waves busy although ray costs differ by 10-100x. Same visit order and
 // the same (t, triangle id) closest-hit rule as traverse<>.
 #ifndef YRT_REFILL
-#define YRT_REFILL 40  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6
+#define YRT_REFILL 48  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6;
+                        // with four lanes 48 over 40: C4 -0.8 %, C3 +0.2 % (r05cc/dd); 56: C3 -1.6 %
 #endif
 #if defined(YRT_PROFILE) && defined(YRT_SHADE_PROF)
 #error "YRT_PROFILE and YRT_SHADE_PROF share the profile counters: build one at a time"
