@@ -375,8 +375,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_raygen(FrameView fv, PathBuffers 
 // This keeps 64-wide waves busy although ray costs differ by 10-100x. Same visit order and
 // the same (t, triangle id) closest-hit rule as traverse<>.
 #ifndef YRT_REFILL
-#define YRT_REFILL 48  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6;
-                        // with four lanes 48 over 40: C4 -0.8 %, C3 +0.2 % (r05cc/dd); 56: C3 -1.6 %
+#define YRT_REFILL 40  // 24/6 +1.3 % over 16/4; with 64-lane blocks 28/6 +0.4 %, then 40/8 +0.9 % over 28/6;
+                        // with four lanes 48 everywhere: C4 -0.8 %, C3 +0.2 %, C5 +1.6 % (r05cc/dd/ee)
 #endif
 #if defined(YRT_PROFILE) && defined(YRT_SHADE_PROF)
 #error "YRT_PROFILE and YRT_SHADE_PROF share the profile counters: build one at a time"
@@ -400,6 +400,9 @@ __device__ unsigned long long g_traceProfile[8];
 
 #ifndef YRT_REFILL_ANY
 #define YRT_REFILL_ANY YRT_REFILL  // refill threshold of the any-hit (shadow) instantiation
+#endif
+#ifndef YRT_REFILL_PRIM
+#define YRT_REFILL_PRIM YRT_REFILL  // refill threshold of the fused depth-0 instantiation
 #endif
 #ifndef YRT_TRI_STEP
 #define YRT_TRI_STEP 2  // triangles per lane per leaf step (0 = whole leaf): 2 is +0.7 % over whole leaves
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
     const int nIdle = __popcll(idle);
     YRT_PROF(0, 1);
     YRT_PROF(1, 64 - nIdle);
-    if (nIdle >= (ANY ? YRT_REFILL_ANY : YRT_REFILL)) {
+    if (nIdle >= (ANY ? YRT_REFILL_ANY : PRIM ? YRT_REFILL_PRIM : YRT_REFILL)) {
       if (next < end) {
         const unsigned li = next + lanes_below(idle);
         if (!has) {
