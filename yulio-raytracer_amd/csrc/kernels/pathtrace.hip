@@ -399,7 +399,7 @@ __device__ unsigned long long g_traceProfile[8];
 #endif
 
 #ifndef YRT_REFILL_ANY
-#define YRT_REFILL_ANY YRT_REFILL  // refill threshold of the any-hit (shadow) instantiation
+#define YRT_REFILL_ANY 32  // any hit: with node bias 20, C3 +1.5 %, C4 / C5 within the spread (r05ii)
 #endif
 #ifndef YRT_REFILL_PRIM
 #define YRT_REFILL_PRIM YRT_REFILL  // refill threshold of the fused depth-0 instantiation
@@ -414,7 +414,9 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
 #ifndef YRT_NODE_BIAS_ANY
-#define YRT_NODE_BIAS_ANY 12  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %
+#define YRT_NODE_BIAS_ANY 20  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %;
+                              // four lanes (r05gg-ii): 24 / 32 C3 -2.0 / -2.8 % but C5 +1.6 / +2.3 %
+                              // unless refill 32 (20 / 32: C3 -1.5 %, C5 +0.0 %)
 #endif
 #ifndef YRT_NODE_UNROLL_ANY
 #define YRT_NODE_UNROLL_ANY 1  // any-hit: node steps between two node/leaf-phase checks
