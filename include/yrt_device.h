@@ -267,6 +267,11 @@ YRT_API int yrtDebugTraceProfile(YRTDevice dev, uint64_t* out8, int reset);
  * reciprocal (rcp_rn, common/yrt_math.h) with the IEEE division 1.0f/x for all 2^32 inputs.
  * out2[0] = mismatches, out2[1] = the smallest mismatching input (or UINT64_MAX). */
 YRT_API int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2);
+/* Arithmetic self-check of the emulated SSE estimates the reference's rcp/rsqrt start from
+ * (common/yrt_sse_rcp.h; common/math/math.h:38-59): fn 1 rcpps, fn 2 rsqrtps, each against its
+ * reconstruction from table2048 (the 12-bit mantissas of tests/golden/sse_rcp_tables.json) for
+ * all 2^32 inputs. out2 as yrtDebugCheckMath. */
+YRT_API int yrtDebugCheckMathTable(YRTDevice dev, int fn, const uint16_t* table2048, uint64_t* out2);
 /* Parity debugging: out4 == NULL arms the capture of the per-sample radiance (the pathL terms
  * the resolve sums, in s order) of pixel id y*width+x (-1 disarms) of frame `frame` for the
  * following renders (buffer of maxSamples float4); out4 != NULL copies the captured samples

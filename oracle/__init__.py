@@ -24,6 +24,8 @@ def build():
 if not LIB.exists():
     build()
 REF_LIB = HERE / "_ref" / "libref_kat.so"  # reference-compiled KAT library (make -C oracle ref)
+REF_MATH_LIB = HERE / "_ref" / "libref_math.so"  # the reference's common/math, compiled (make -C oracle ref)
+IEEE_LIB = HERE / "liboracle_ieee.so"  # rcp = 1/x, rsqrt = 1/sqrt(x): tools/rcp_sensitivity.py only
 _lib = C.CDLL(str(LIB))
 
 vp, sz, i32, PF = C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_float)
@@ -56,6 +58,9 @@ _sig("oracle_random_floats", None, i32, i32, vp)
 _sig("oracle_permutations", None, i32, i32, i32, vp)
 _sig("oracle_shuffles", None, i32, i32, i32, vp)
 _sig("oracle_libm", None, i32, i32, vp, vp, vp)
+_sig("oracle_vecmath", None, i32, i32, vp, vp, vp)
+_sig("oracle_bsphere", None, i32, vp, vp, vp, vp, vp)
+_sig("oracle_camera_rays", i32, vp, sz, i32, vp, vp, vp)
 
 
 def _err():
@@ -63,14 +68,29 @@ def _err():
     return e.decode() if e else "?"
 
 
-def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0):
+_ieee = None
+
+
+def _ieee_lib():
+    """liboracle_ieee.so: the same restatement with rcp = 1/x, rsqrt = 1/sqrt(x) (the substitution
+    of rounds 1-5), for tools/rcp_sensitivity.py."""
+    global _ieee
+    if _ieee is None:
+        _ieee = C.CDLL(str(IEEE_LIB))
+        _ieee.oracle_render.restype = i32
+        _ieee.oracle_render.argtypes = _lib.oracle_render.argtypes
+    return _ieee
+
+
+def render(blob: bytes, width, height, gamma=1.0, rect=None, threads=0, ieee_rcp=False):
     """RGB_FLOAT32 image (H, W, 3) of the frame blob; pixels outside rect stay NaN."""
     threads = threads or cpu_count()
     x0, y0, x1, y1 = rect if rect is not None else (0, 0, width, height)
     out = np.full((height, width, 3), np.nan, np.float32)
     st = OracleStats()
-    rc = _lib.oracle_render(blob, len(blob), width, height, gamma, x0, y0, x1, y1, threads, out.ctypes.data,
-                            C.byref(st))
+    lib = _ieee_lib() if ieee_rcp else _lib
+    rc = lib.oracle_render(blob, len(blob), width, height, gamma, x0, y0, x1, y1, threads, out.ctypes.data,
+                           C.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle_render: {_err()}")
     return out, {n: getattr(st, n) for n, _ in st._fields_}
@@ -159,6 +179,40 @@ def libm(fn, x, y=None):
     out = np.zeros_like(x)
     _lib.oracle_libm(LIBM[fn], x.size, x.ctypes.data, y.ctypes.data, out.ctypes.data)
     return out
+
+
+VECMATH = {"dot": (0, 3, 3, 1), "cross": (1, 3, 3, 3), "normalize": (2, 3, 0, 3), "length": (3, 3, 0, 1),
+           "lmul": (4, 9, 3, 3), "frame": (5, 3, 0, 9), "inverse": (6, 9, 0, 9), "color_div": (7, 3, 1, 3),
+           "rcp": (8, 1, 0, 1), "rsqrt": (9, 1, 0, 1), "rcpps": (10, 1, 0, 1), "rsqrtps": (11, 1, 0, 1)}
+
+
+def vecmath(name, a, b=None):
+    """The oracle's vector helper `name` element-wise (VECMATH: fn, floats per item of a, of b, of out)."""
+    fn, na, nb, no = VECMATH[name]
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, na)
+    n = a.shape[0]
+    b = np.zeros((n, max(nb, 1)), np.float32) if b is None else np.ascontiguousarray(b, np.float32).reshape(n, -1)
+    out = np.zeros((n, no), np.float32)
+    _lib.oracle_vecmath(fn, n, a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out if no > 1 else out[:, 0]
+
+
+def bsphere(lo, hi, org, dir_):
+    """AmbientLight's bounding sphere intersection: (n, 4) hit, near, far, radius."""
+    arrs = [np.ascontiguousarray(x, np.float32).reshape(-1, 3) for x in (lo, hi, org, dir_)]
+    out = np.zeros((arrs[0].shape[0], 4), np.float32)
+    _lib.oracle_bsphere(arrs[0].shape[0], *[x.ctypes.data for x in arrs], out.ctypes.data)
+    return out
+
+
+def camera_rays(blob: bytes, px):
+    """The frame blob camera's rays for pixel coordinates px (n, 2) = (fx, fy): org, dir (n, 3)."""
+    px = np.ascontiguousarray(px, np.float32).reshape(-1, 2)
+    org = np.zeros((px.shape[0], 3), np.float32)
+    dir_ = np.zeros_like(org)
+    if _lib.oracle_camera_rays(blob, len(blob), px.shape[0], px.ctypes.data, org.ctypes.data, dir_.ctypes.data):
+        raise RuntimeError(f"oracle_camera_rays: {_err()}")
+    return org, dir_
 
 
 def permutations(size, seed, count):

@@ -5,6 +5,8 @@
 
 /* the per-ray path's elementary functions, evaluated exactly as the device does */
 #include "../yulio-raytracer_amd/csrc/common/yrt_libm.h"
+/* the reference's rcp/rsqrt: Intel rcpps/rsqrtps emulated exactly + math.h's Newton step */
+#include "../yulio-raytracer_amd/csrc/common/yrt_sse_rcp.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -23,7 +25,9 @@ static int fail(const char* msg) {
 }
 
 /* ====================================================================== vector math
- * common/math/vec3.h, linearspace3.h, affinespace.h; rcp -> 1/x, rsqrt -> 1/sqrt(x). */
+ * common/math/vec3.h, linearspace3.h, affinespace.h; rcp and rsqrt as common/math/math.h:38-59
+ * (the SSE estimate + one Newton step, yrt_sse_rcp.h); -DYRT_ORACLE_IEEE_RCP builds the round 1-5
+ * substitution (1/x, 1/sqrt(x)) for the sensitivity measurement (tools/rcp_sensitivity.py). */
 typedef struct { float x, y, z; } V3;
 static inline V3 v3(float x, float y, float z) { V3 r = {x, y, z}; return r; }
 static inline V3 vs(float s) { return v3(s, s, s); }
@@ -40,8 +44,13 @@ static inline V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
  *   lmul  = v.x*vx + v.y*vy + v.z*vz left to right, common/math/linearspace3.h:134. */
 static inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static inline V3 cross(V3 a, V3 b) { return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+#if defined(YRT_ORACLE_IEEE_RCP)
 static inline float rcp(float x) { return 1.0f / x; }
 static inline float rsqrt_(float x) { return 1.0f / sqrtf(x); }
+#else
+static inline float rcp(float x) { return yrt_ref_rcp(x); }      /* math.h:38-42 */
+static inline float rsqrt_(float x) { return yrt_ref_rsqrt(x); } /* math.h:53-58 */
+#endif
 static inline V3 normalize(V3 a) { return muls(a, rsqrt_(dot(a, a))); }
 static inline float length(V3 a) { return sqrtf(dot(a, a)); }
 static inline float fmax3(V3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
@@ -1163,6 +1172,76 @@ void oracle_libm(int fn, int n, const float* x, const float* y, float* out) {
     }
   }
 }
+/* The vector helpers, element-wise, for the pin against the reference's own common/math
+ * (tests/test_ref_pin.py, oracle/ref_math.cpp ref_vec: same fn numbers and layouts):
+ * 0 dot, 1 cross, 2 normalize, 3 length, 4 L * v (9 floats, columns), 5 frame, 6 inverse,
+ * 7 Color / float (color_sse.h:162: a * rcp(b)), 8 rcp, 9 rsqrt, 10 rcpps, 11 rsqrtps (x = a) */
+void oracle_vecmath(int fn, int n, const float* a, const float* b, float* out) {
+#define V3P(p) v3((p)[0], (p)[1], (p)[2])
+#define PUT3(o, v) ((o)[0] = (v).x, (o)[1] = (v).y, (o)[2] = (v).z)
+  for (int i = 0; i < n; ++i) {
+    const float* A = a + (fn == 4 || fn == 6 ? 9 : fn >= 8 ? 1 : 3) * i;
+    switch (fn) {
+      case 0: out[i] = dot(V3P(A), V3P(b + 3 * i)); break;
+      case 1: { const V3 r = cross(V3P(A), V3P(b + 3 * i)); PUT3(out + 3 * i, r); break; }
+      case 2: { const V3 r = normalize(V3P(A)); PUT3(out + 3 * i, r); break; }
+      case 3: out[i] = length(V3P(A)); break;
+      case 4: { const V3 r = lmul(l3(V3P(A), V3P(A + 3), V3P(A + 6)), V3P(b + 3 * i)); PUT3(out + 3 * i, r); break; }
+      case 5: {
+        const L3 f = frame_(V3P(A));
+        PUT3(out + 9 * i, f.vx); PUT3(out + 9 * i + 3, f.vy); PUT3(out + 9 * i + 6, f.vz);
+        break;
+      }
+      case 6: {
+        const L3 f = linv(l3(V3P(A), V3P(A + 3), V3P(A + 6)));
+        PUT3(out + 9 * i, f.vx); PUT3(out + 9 * i + 3, f.vy); PUT3(out + 9 * i + 6, f.vz);
+        break;
+      }
+      case 7: { const V3 r = muls(V3P(A), rcp(b[i])); PUT3(out + 3 * i, r); break; }
+      case 8: out[i] = rcp(A[0]); break;
+      case 9: out[i] = rsqrt_(A[0]); break;
+      case 10: out[i] = yrt_rcpps(A[0]); break;
+      default: out[i] = yrt_rsqrtps(A[0]); break;
+    }
+  }
+#undef V3P
+#undef PUT3
+}
+
+/* AmbientLight's bounding sphere (lights/ambientlight.h:44,71, restated for the pin only: the
+ * integrator overwrites the shadow ray's tMax with tMaxShadowRay, pathtraceintegrator.cpp:151,
+ * so no render reads it): getBSphere (common/math/bbox.h:75-78), BSphere::rayIntersect
+ * (common/math/bsphere.h:93-100), solveQuadratic (common/math/math.h:174-208).
+ * out[4i] = hit, near, far, radius */
+void oracle_bsphere(int n, const float* lo, const float* hi, const float* org, const float* dir, float* out) {
+  for (int i = 0; i < n; ++i) {
+    const V3 L = v3(lo[3 * i], lo[3 * i + 1], lo[3 * i + 2]), H = v3(hi[3 * i], hi[3 * i + 1], hi[3 * i + 2]);
+    const V3 c = muls(add(L, H), 0.5f);
+    const float radius = length(sub(c, H));
+    const V3 o = sub(v3(org[3 * i], org[3 * i + 1], org[3 * i + 2]), c);
+    const V3 d = v3(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    const float qa = dot(d, d), qb = 2 * dot(o, d), qc = dot(o, o) - radius * radius;
+    int hit = 0;
+    float x0 = 0.f, x1 = 0.f;
+    if (qa == 0) {
+      if (qb != 0) { x0 = x1 = -qc / qb; hit = 1; }
+    } else {
+      const float disc = qb * qb - 4.0f * qa * qc;
+      if (!(disc < 0)) {
+        const float sd = sqrtf(disc);
+        const float tmp = qb < 0 ? -0.5f * (qb - sd) : -0.5f * (qb + sd);
+        x0 = tmp / qa;
+        x1 = qc / tmp;
+        if (x0 > x1) { const float t = x0; x0 = x1; x1 = t; }
+        hit = 1;
+      }
+    }
+    out[4 * i] = (float)hit;
+    out[4 * i + 1] = hit ? x0 : 0.f;
+    out[4 * i + 2] = hit ? x1 : 0.f;
+    out[4 * i + 3] = radius;
+  }
+}
 void oracle_random_floats(int seed, int n, float* out) {
   Rnd r;
   rnd_seed(&r, seed);
@@ -1633,18 +1712,21 @@ static V3 micro_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const float G = fminf(fminf(1.0f, 2.0f * cH * cO * rcp(cT)), 2.0f * cH * cI * rcp(cT));
   return muls(mulv(muls(muls(c->R, D), G), F), rcp(4.0f * cO));
 }
-/* Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26) */
+/* Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26). Color / float is
+ * a * rcp(b) in the reference (common/math/color_sse.h:162), not a division. */
+static V3 col_divs(V3 a, float s) { return muls(a, rcp(s)); }
+/* Vector3f / float: _mm_div_ps (vector3f_sse.h:155), an IEEE division */
 static V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
 static V3 minnaert_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const float cI = clamp01(dot(wi, dg->Ns));
   const float bs = yrt_powf(clamp01(dot(wo, wi)), c->a);
-  return divs(muls(muls(c->R, bs), cI), PI_F);
+  return col_divs(muls(muls(c->R, bs), cI), PI_F);
 }
 static V3 velvety_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
   const float cO = clamp01(dot(wo, dg->Ns)), cI = clamp01(dot(wi, dg->Ns));
   const float sO = sqrtf(1.0f - cO * cO);
   const float hs = yrt_powf(sO, c->a);
-  return divs(muls(muls(c->R, hs), cI), PI_F);
+  return col_divs(muls(muls(c->R, hs), cI), PI_F);
 }
 /* DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38) */
 static V3 layer_eval(const Brdf* c, V3 wo, const DG* dg, V3 wi) {
@@ -2310,6 +2392,23 @@ static void* worker(void* arg) {
 }
 
 /* DebugRenderer::RenderJob::renderTile (debugrenderer.cpp:66-140) */
+/* The frame blob's camera rays for pixel coordinates px[2i] = fx, px[2i+1] = fy (lens sample 0):
+ * org[3i], dir[3i]. For the pin of the camera path against the reference's own operations. */
+int oracle_camera_rays(const void* blob, size_t bytes, int n, const float* px, float* org, float* dir) {
+  Blob B;
+  if (blob_parse(blob, bytes, &B)) return -1;
+  Camera C;
+  if (camera_build(&B, &C)) { blob_free(&B); return -1; }
+  for (int i = 0; i < n; ++i) {
+    V3 o, d;
+    camera_ray(&C, px[2 * i], px[2 * i + 1], 0.f, 0.f, &o, &d);
+    org[3 * i] = o.x; org[3 * i + 1] = o.y; org[3 * i + 2] = o.z;
+    dir[3 * i] = d.x; dir[3 * i + 1] = d.y; dir[3 * i + 2] = d.z;
+  }
+  blob_free(&B);
+  return 0;
+}
+
 static void debug_render(const World* W, const RCfg* R, const Camera* C, int width, int height, float* out) {
   const int ntx = (width + 15) / 16, nty = (height + 15) / 16;
   const float rcpW = rcp((float)width), rcpH = rcp((float)height);

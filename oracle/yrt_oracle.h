@@ -91,6 +91,11 @@ void oracle_random_ints(int seed, int n, int32_t* out);
 void oracle_random_floats(int seed, int n, float* out);
 /* yrt_libm.h functions (fn 0 sin 1 cos 2 exp 3 log 4 pow(x,y) 5 asin 6 acos 7 atan 8 atan2(x,y)) */
 void oracle_libm(int fn, int n, const float* x, const float* y, float* out);
+/* the vector helpers and the camera path for the pin against the reference's common/math
+ * (oracle/ref_math.cpp, tests/test_ref_pin.py) */
+void oracle_vecmath(int fn, int n, const float* a, const float* b, float* out);
+void oracle_bsphere(int n, const float* lo, const float* hi, const float* org, const float* dir, float* out);
+int oracle_camera_rays(const void* blob, size_t bytes, int n, const float* px, float* org, float* dir);
 void oracle_permutations(int size, int seed, int count, int32_t* out);
 void oracle_shuffles(int n, int seed, int count, uint32_t* out);
 /* SamplerFactory::init sample table: dims as in the GPU table ([dim][set*spp+s]);

@@ -51,6 +51,24 @@ def test_fast_reciprocal_is_correctly_rounded(gpu_device):
     assert out[0] == 0, f"{out[0]} mismatches, first input bits {out[1]:#x}"
 
 
+@pytest.mark.parametrize("fn,key", [(1, "rcpps_mantissa12"), (2, "rsqrtps_mantissa12")])
+def test_sse_estimates_match_the_intel_tables(gpu_device, fn, key):
+    """The kernels' emulation of rcpps / rsqrtps (the estimates the reference's rcp/rsqrt start
+    from, common/math/math.h:38-59; yrt_sse_rcp.h) equals the committed Intel tables
+    (tests/golden/sse_rcp_tables.json) on all 2^32 inputs: the GPU computes the reference's
+    reciprocals bit for bit, like the host and the oracle (tests/test_sse_rcp.py,
+    tests/test_ref_pin.py)."""
+    import ctypes as C
+    import json
+    from pathlib import Path
+    from yrt import _native as N
+    fix = json.loads((Path(__file__).resolve().parent / "golden" / "sse_rcp_tables.json").read_text())
+    tab = np.ascontiguousarray(fix[key], np.uint16)
+    out = (C.c_uint64 * 2)()
+    assert N.dev.yrtDebugCheckMathTable(gpu_device.h, fn, tab.ctypes.data, out) == 0, gpu_device.error()
+    assert out[0] == 0, f"{out[0]} mismatches, first input bits {out[1]:#x}"
+
+
 # ----------------------------------------------------------------------------- ray queries
 def _rays(blob, n, seed=42):
     """SURVEY §8(d)(ii) incoherent rays: origins uniform in the scene AABB, directions on S^2."""

@@ -6,16 +6,17 @@
 //   LinearSpace3 * v = v.x*vx + v.y*vy + v.z*vz  common/math/linearspace3.h:134
 //   AffineSpace3 products / lookAtPoint / rotate common/math/affinespace.h:60-78,
 //                                                common/math/linearspace3.h:95-101
-// The reference's rcp/rsqrt are SSE rcpps/rsqrtps + one Newton step (math.h:38-59),
-// vendor-specific in the last bits; here rcp(x) = 1/x and rsqrt(x) = 1/sqrt(x), both
-// IEEE correctly rounded on host and on gfx950 (the difference is part of the stated
-// parity tolerance).
+// rcp/rsqrt are the reference's own: the Intel SSE estimate (rcpps/rsqrtps, emulated exactly
+// with integer arithmetic, yrt_sse_rcp.h) plus the Newton step of common/math/math.h:38-59, on
+// host and gfx950 alike. -DYRT_IEEE_RCP restores round 1-5's substitution (correctly rounded
+// 1/x and 1/sqrt(x)) for A/B measurements.
 #pragma once
 
 #include <math.h>
 #include <stdint.h>
 
 #include "yrt_libm.h"
+#include "yrt_sse_rcp.h"
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -78,11 +79,18 @@ __host__ __device__ __forceinline__ float rcp_rn(float x) {
   return 1.0f / x;
 #endif
 }
+#endif
+#if defined(YRT_IEEE_RCP)
+#if defined(__HIPCC__)
 YRT_HD float rcpf_(float x) { return rcp_rn(x); }
 YRT_HD float rsqrtf_(float x) { return rcp_rn(sqrtf(x)); }
 #else
 YRT_HD float rcpf_(float x) { return 1.0f / x; }
 YRT_HD float rsqrtf_(float x) { return 1.0f / sqrtf(x); }
+#endif
+#else
+YRT_HD float rcpf_(float x) { return yrt_ref_rcp(x); }    // common/math/math.h:38-42
+YRT_HD float rsqrtf_(float x) { return yrt_ref_rsqrt(x); }  // common/math/math.h:53-58
 #endif
 YRT_HD V3 normalize(V3 a) { return a * rsqrtf_(dot(a, a)); }
 YRT_HD float length(V3 a) { return sqrtf(dot(a, a)); }

@@ -834,7 +834,12 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     // YRT_PRIMARY=0: never, 2: always.
     const int primMode = getenv("YRT_PRIMARY") ? atoi(getenv("YRT_PRIMARY")) : 1;
     const double primMiss = getenv("YRT_PRIMARY_MISS") ? atof(getenv("YRT_PRIMARY_MISS")) : 0.5;
-    const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 && primMode != 0;
+    // Toe-in stereo cameras (the DLL's FPR default) are left to k_raygen: the fused kernel is
+    // compiled without that branch (camera_ray<false>, pathtrace.hip).
+    bool toeIn = false;
+    for (const GpuCamera& c : g.hCams) toeIn |= c.type == CAM_STEREO && c.toeIn != 0;
+    const bool fusedPrimary = captureMax == 0 && !G.hasMotion && !fv.backplateTexels && sv.numEnvDir == 0 &&
+                              primMode != 0 && !toeIn;
     // A lane's batch is enqueued a step at a time — its prologue (counter clear, camera rays),
     // one depth (closest trace, shade, shadow trace), its epilogue (counter copy, pixel resolve)
     // — round-robin over the lanes that hold a batch, so every lane's first kernels are queued
@@ -2010,6 +2015,15 @@ int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2) {
   if (fn != 0 || !out2) throw std::runtime_error("yrtDebugCheckMath: fn 0 only");
   HIP_CHECK(hipSetDevice(dev->d->hipDevice));
   if (check_math(fn, (unsigned long long*)out2) != 0) throw std::runtime_error("check_math failed");
+  return 0;
+  DEV_END(-1)
+}
+
+int yrtDebugCheckMathTable(YRTDevice dev, int fn, const uint16_t* table2048, uint64_t* out2) {
+  DEV_GUARD(dev, -1)
+  if ((fn != 1 && fn != 2) || !table2048 || !out2) throw std::runtime_error("yrtDebugCheckMathTable: fn 1 or 2");
+  HIP_CHECK(hipSetDevice(dev->d->hipDevice));
+  if (check_math_table(fn, table2048, (unsigned long long*)out2) != 0) throw std::runtime_error("check_math_table failed");
   return 0;
   DEV_END(-1)
 }

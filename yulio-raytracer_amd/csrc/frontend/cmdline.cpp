@@ -16,16 +16,21 @@
 #include <stdexcept>
 
 #include "frontend.h"
+#include "../common/yrt_sse_rcp.h"
 
 namespace yrtfe {
 
+// AffineSpace3f::lookAtPoint (common/math/affinespace.h:72-77) in the reference's Vector3f
+// operations: dot = (x*x + y*y) + z*z (_mm_dp_ps), normalize = a * rsqrt(dot) with the SSE
+// rsqrt sequence of common/math/math.h:53-58 (yrt_sse_rcp.h); pinned against the reference's own
+// headers by tests/test_ref_pin.py::test_front_end_camera_basis.
 yrt_affine look_at(yrt_v3 eye, yrt_v3 point, yrt_v3 up) {
   auto sub = [](yrt_v3 a, yrt_v3 b) { return yrt_v3{a.x - b.x, a.y - b.y, a.z - b.z}; };
   auto cross = [](yrt_v3 a, yrt_v3 b) {
     return yrt_v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
   };
   auto norm = [](yrt_v3 a) {
-    const float r = 1.0f / sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+    const float r = yrt_ref_rsqrt(a.x * a.x + a.y * a.y + a.z * a.z);
     return yrt_v3{a.x * r, a.y * r, a.z * r};
   };
   const yrt_v3 Z = norm(sub(point, eye));

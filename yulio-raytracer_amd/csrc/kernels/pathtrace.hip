@@ -182,7 +182,12 @@ __device__ __forceinline__ void pinhole_ray(const CAM& cam, float fx, float fy, 
   org = p2w.p;
   dir = normalize(fx * p2w.l.vx + (1.0f - fy) * p2w.l.vy + p2w.l.vz);
 }
-template <class CAM>  // GpuCamera, or a YRT_CONST one (scalar loads)
+// TOEIN = false drops the toe-in stereo branch: the fused depth-0 trace kernel takes no toe-in
+// camera (the host routes those frames through k_raygen). Its two rotations about per-ray
+// points and the reference's rcp/rsqrt sequences need ~40 more VGPRs than the rest of the
+// camera code (k_raygen 37 -> 76), which at the fused kernel's 96-VGPR cap spilled 60-76 B
+// into its traversal loop.
+template <bool TOEIN = true, class CAM>  // GpuCamera, or a YRT_CONST one (scalar loads)
 __device__ void camera_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir, float lx = 0.f,
                            float ly = 0.f) {
   if (cam.type == CAM_PINHOLE) {
@@ -227,7 +232,7 @@ __device__ void camera_ray(const CAM& cam, float fx, float fy, V3& org, V3& dir,
     const float coef = 1.f - smoothstepf(0.f, 1.f, smoothstepf(cam.falloffAngle, 90.f, absoluteVerticalAngle));
     eyeOffset *= coef;
   }
-  if (cam.toeIn) {
+  if (TOEIN && cam.toeIn) {
     p2w = mul(p2w, a3_translate(v3(eyeOffset, 0.f, 0.f)));
     const V3 origin = ld3(cam.origin), up = ld3(cam.up);
     const A3 rayRotationSpace = a3_rotate_about(origin, up, theta);
@@ -634,7 +639,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                   const int f0 = __builtin_amdgcn_readfirstlane(f);
                   if (f == f0) {
                     const YRT_CONST GpuCamera& cam = const_ref(pr.fv.cam + f0);
-                    camera_ray(cam, fx, fy, o3, d3, lx, ly);
+                    camera_ray<false>(cam, fx, fy, o3, d3, lx, ly);
                     todo = false;
                   }
                 }
@@ -2055,6 +2060,64 @@ __global__ __launch_bounds__(256) void k_check_math(int fn, unsigned long long* 
     atomicAdd(&out[0], bad);
     atomicMin(&out[1], first);
   }
+}
+
+// fn 1 / 2: the emulated SSE estimates yrt_rcpps / yrt_rsqrtps (common/yrt_sse_rcp.h) against a
+// reconstruction from the 2048-entry table `tab` of 12-bit mantissas (the Intel fixture,
+// tests/golden/sse_rcp_tables.json), for every 32-bit pattern; written independently of the
+// emulation (the reconstruction of tests/test_sse_rcp.py).
+__device__ __forceinline__ uint32_t sse_expect(int fn, uint32_t u, const uint16_t* tab) {
+  const uint32_t s = u >> 31, e = (u >> 23) & 0xffu, mant = u & 0x7fffffu;
+  if (fn == 1) {
+    if (e == 0u) return (s << 31) | 0x7f800000u;
+    if (e == 255u) return mant ? (u | 0x400000u) : (s << 31);
+    if (e >= 253u) return s << 31;
+    return (s << 31) | ((253u - e) << 23) | ((uint32_t)tab[(u >> 12) & 0x7ffu] << 11);
+  }
+  if (e == 0u) return (s << 31) | 0x7f800000u;
+  if (e == 255u && mant) return u | 0x400000u;
+  if (s) return 0xffc00000u;
+  if (e == 255u) return 0u;
+  const int E = (int)e - 127, p = E & 1, k = (E - p) / 2;
+  return ((uint32_t)(126 - k) << 23) | ((uint32_t)tab[((uint32_t)p << 10) | ((u >> 13) & 0x3ffu)] << 11);
+}
+__global__ __launch_bounds__(256) void k_check_math_table(int fn, const uint16_t* __restrict__ tab,
+                                                          unsigned long long* out) {
+  unsigned long long bad = 0, first = ~0ull;
+  for (unsigned long long i = blockIdx.x * 256ull + threadIdx.x; i < (1ull << 32);
+       i += (unsigned long long)gridDim.x * 256ull) {
+    const uint32_t u = (uint32_t)i;
+    const float x = __uint_as_float(u);
+    const uint32_t got = __float_as_uint(fn == 1 ? yrt_rcpps(x) : yrt_rsqrtps(x));
+    if (got != sse_expect(fn, u, tab)) {
+      ++bad;
+      first = i < first ? i : first;
+    }
+  }
+  if (bad) {
+    atomicAdd(&out[0], bad);
+    atomicMin(&out[1], first);
+  }
+}
+
+int check_math_table(int fn, const uint16_t* table2048, unsigned long long* host2) {
+  if (fn != 1 && fn != 2) return -1;
+  unsigned long long* d = nullptr;
+  uint16_t* t = nullptr;
+  if (hipMalloc(&d, 16) != hipSuccess) return -1;
+  if (hipMalloc(&t, 4096) != hipSuccess) { (void)hipFree(d); return -1; }
+  const unsigned long long init[2] = {0ull, ~0ull};
+  int rc = 0;
+  if (hipMemcpy(d, init, 16, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(t, table2048, 4096, hipMemcpyHostToDevice) != hipSuccess)
+    rc = -1;
+  if (!rc) {
+    hipLaunchKernelGGL(k_check_math_table, dim3(8192), dim3(256), 0, 0, fn, t, d);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host2, d, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+  }
+  (void)hipFree(t);
+  (void)hipFree(d);
+  return rc;
 }
 
 int check_math(int fn, unsigned long long* host2) {

@@ -178,6 +178,7 @@ int trace_profile(unsigned long long* out8, int reset);
 int debug_pixel_capture(int pixelId, int frame, float4* out, int capacity);
 // Arithmetic self-check of the correctly rounded fast reciprocal (rcp_rn): see pathtrace.hip
 int check_math(int fn, unsigned long long* host2);
+int check_math_table(int fn, const uint16_t* table2048, unsigned long long* host2);
 // Multi-GPU gather (device.cpp): the pixels of the tiles of one shard (job tile =
 // tileOffset + j * tileStride, j < numTiles, over numFrames stacked frames of tilesPerFrame
 // tiles) as a slab of numTiles * 256 elements in tile order j and scan order within the tile;

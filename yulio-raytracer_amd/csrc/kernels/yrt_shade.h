@@ -359,18 +359,19 @@ __device__ __forceinline__ V3 glitter_layer_eval(const Comp& c, V3 wo, const DG&
   return Fo * v3s(1.0f) * Fg * v3s(1.0f) * Fi;
 }
 
-// Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26)
+// Minnaert::eval (brdfs/minnaert.h:20-24), Velvety::eval (brdfs/velvety.h:20-26). Color / float
+// is a * rcp(b) in the reference (common/math/color_sse.h:162), not a division.
 __device__ __forceinline__ V3 minnaert_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   const float cosThetaI = clampf(dot(wi, dg.Ns));
   const float backScatter = yrt_powf(clampf(dot(wo, wi)), c.a);
-  return c.R * backScatter * cosThetaI / kPi;
+  return c.R * backScatter * cosThetaI * rcpf_(kPi);
 }
 __device__ __forceinline__ V3 velvety_eval(const Comp& c, V3 wo, const DG& dg, V3 wi) {
   const float cosThetaO = clampf(dot(wo, dg.Ns));
   const float cosThetaI = clampf(dot(wi, dg.Ns));
   const float sinThetaO = sqrtf(1.0f - cosThetaO * cosThetaO);
   const float horizonScatter = yrt_powf(sinThetaO, c.a);
-  return c.R * horizonScatter * cosThetaI / kPi;
+  return c.R * horizonScatter * cosThetaI * rcpf_(kPi);
 }
 
 // DielectricLayer<Lambertian>::eval (brdfs/dielectriclayer.h:27-38), T = one

@@ -166,6 +166,7 @@ _sig(dev, "yrtGetCapturedRays", C.c_int64, vp, i32, i32, vp, vp, sz, C.POINTER(C
 _sig(dev, "yrtDebugTraceProfile", i32, vp, C.POINTER(C.c_uint64), i32)
 try:  # debug-only entry; absent from older tuning builds selected with YRT_LIB_DIR
     _sig(dev, "yrtDebugCheckMath", i32, vp, i32, C.POINTER(C.c_uint64))
+    _sig(dev, "yrtDebugCheckMathTable", i32, vp, i32, vp, C.POINTER(C.c_uint64))
     _sig(dev, "yrtDebugPixelSamples", i32, vp, i32, i32, vp, i32)
 except AttributeError:
     pass
