@@ -73,7 +73,10 @@ YULIO_DLL_EXPORT void InitParamsRT(ParamsRT* params);
 
 }  // namespace Yulio
 
-/* Global names for callers of this build that predate the namespace (the same entities). */
+/* Global names for callers of this build that predate the namespace (the same entities): opt-in
+ * with -DYULIO_RT_GLOBAL_NAMES, since the reference header keeps them inside namespace Yulio only
+ * and names such as Done or NoError would clash with other libraries' globals. */
+#if defined(YULIO_RT_GLOBAL_NAMES)
 using Yulio::ErrorCodeRT;
 using Yulio::NoError;
 using Yulio::RenderingIsInProgress;
@@ -96,6 +99,7 @@ using Yulio::StopRT;
 using Yulio::GetLastErrorRT;
 using Yulio::GetCurrentStatusRT;
 using Yulio::InitParamsRT;
+#endif
 
 #else /* C */
 

@@ -36,7 +36,7 @@ static_assert(sizeof(GpuNode) == 128, "node is one 128-B line");
 struct GpuTri {
   float v0[4];  // xyz, w = global triangle id (bits)
   float e1[4];  // xyz, w = flags (bits): bit0 cullBackFaces
-  float e2[4];  // xyz, w unused
+  float e2[4];  // xyz, w = geometry id (bits): the closest-hit kernels store it beside the hit
 };
 static_assert(sizeof(GpuTri) == 48, "tri record size");
 

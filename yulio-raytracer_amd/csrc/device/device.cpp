@@ -52,7 +52,7 @@ struct GpuCtx {
   // latency-bound shading).
   struct Lane {
     hipStream_t stream = nullptr;
-    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
+    DevBuf qPath[2], qOrg[2], qDir[2], qThr[2], hit, hitGeom, pathL, shFirst, sOrg, sDir, sContrib, sOcc, counters, spill;
     DevBuf qTime[2], sTime;  // ray times (moving scenes only)
     int64_t pathCap = 0, shadowCap = 0;
     // Batches enqueued whose queue counters are not yet accounted, oldest first: a pinned
@@ -128,8 +128,15 @@ struct GpuCtx {
 
   GpuCtx(int dev, int lanesWanted) : hipDevice(dev), numLanes(lanesWanted) {
     HIP_CHECK(hipSetDevice(hipDevice));
-    for (Lane& L : lanes) HIP_CHECK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+    ensure_streams(1);
     stream = lanes[0].stream;
+  }
+  // A lane's stream is created when a render first uses the lane: several contexts
+  // in one process (e.g. devices=[0,0]) all map their lanes onto the process's 4 hardware queues
+  // (GPU_MAX_HW_QUEUES), so streams nobody renders on only add to that sharing.
+  void ensure_streams(int n) {
+    for (int l = 0; l < n && l < kMaxLanes; ++l)
+      if (!lanes[l].stream) HIP_CHECK(hipStreamCreateWithFlags(&lanes[l].stream, hipStreamNonBlocking));
   }
   ~GpuCtx() {
     (void)hipSetDevice(hipDevice);
@@ -163,6 +170,7 @@ struct GpuCtx {
         L.qThr[k].alloc(Q * 16);
       }
       L.hit.alloc(Q * 16);
+      L.hitGeom.alloc(Q * 4);
       L.pathL.alloc(Q * 16);
       L.pathCap = Q;
     }
@@ -436,7 +444,13 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
           xb.erase(std::remove_if(xb.begin(), xb.end(), [](const std::weak_ptr<GpuCtx::FrameBlock>& w) {
                      return w.expired();
                    }), xb.end());
-          if (g0.blk && 2 + (int)xb.size() >= GpuCtx::kMaxFrameBlocks) {
+          // blocks alive: blk, spareBlk and the extra ones (spareBlk is usually one of those)
+          int live = (g0.blk ? 1 : 0) + (g0.spareBlk ? 1 : 0);
+          for (const auto& w : xb) {
+            const auto b = w.lock();
+            live += b && b != g0.blk && b != g0.spareBlk;
+          }
+          if (g0.blk && live >= GpuCtx::kMaxFrameBlocks) {
             read_back_block(g0.blk.get());
           } else {
             g0.blk = std::make_shared<GpuCtx::FrameBlock>();
@@ -726,6 +740,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     const size_t counterWords = qcounter_words(levels) + 1;
     const size_t tracedWord = counterWords - 1;
     g.dAccu.alloc((size_t)nf * W * H * 16);
+    g.ensure_streams(nl);
     for (int l = 0; l < nl; ++l) {
       GpuCtx::Lane& L = g.lanes[l];
       GpuCtx::ensure_paths(L, std::max<int64_t>(P, 256ll * spp), numDirect, G.hasMotion);
@@ -758,6 +773,7 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
         pb.qThr[k] = L.qThr[k].as<float4>();
       }
       pb.hit = L.hit.as<float4>();
+      pb.hitGeom = L.hitGeom.as<int>();
       pb.pathL = L.pathL.as<float4>();
       pb.shFirst = L.shFirst.as<int>();
       pb.sOrg = L.sOrg.as<float4>();
@@ -886,10 +902,10 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
           pr.segCap = pb.segCap;
           pr.traced = pb.counters + tracedWord;
           pr.numPaths = (long long)bi.numPixels * spp;
-          launch_trace_primary(lsv, pr, pb.hit, st);
+          launch_trace_primary(lsv, pr, pb.hit, pb.hitGeom, st);
         } else {
           launch_trace_closest(lsv, pb.qOrg[cur], pb.qDir[cur], pb.counters + qcounter_index(d, 0, 0), YRT_QSEGS,
-                               pb.segCap, pb.hit, st, pb.qTime[cur]);
+                               pb.segCap, pb.hit, st, pb.qTime[cur], pb.hitGeom);
         }
         if (kernelTiming) { HIP_CHECK(hipEventRecord(e1.b, st)); evs.push_back(e1); }
         if (captureMax > 0 && J.first == 0)
@@ -974,7 +990,8 @@ void Device::render_shard(GpuCtx& g, GpuScene& G, RendererObj& R, const std::vec
     for (auto e : g.eventPool) (void)hipEventDestroy(e);
     g.eventPool.clear();
   }
-  for (int l = 0; l < GpuCtx::kMaxLanes; ++l) HIP_CHECK(hipStreamSynchronize(g.lanes[l].stream));
+  for (int l = 0; l < GpuCtx::kMaxLanes; ++l)
+    if (g.lanes[l].stream) HIP_CHECK(hipStreamSynchronize(g.lanes[l].stream));
   g.stats.samples = (double)nf * W * H * (R.debug ? 1 : rp.spp);
 }
 
@@ -1845,7 +1862,8 @@ int yrtSetKernelTiming(YRTDevice dev, int enable) {
 }
 int yrtSetLanes(YRTDevice dev, int lanes) {
   DEV_GUARD(dev, -1)
-  if (lanes < 0 || lanes > GpuCtx::kMaxLanes) throw std::runtime_error("yrtSetLanes: 1..4 lanes, 0 = default");
+  if (lanes < 0 || lanes > GpuCtx::kMaxLanes)
+    throw std::runtime_error("yrtSetLanes: 1.." + std::to_string(GpuCtx::kMaxLanes) + " lanes (YRT_MAX_LANES), 0 = default");
   for (auto& c : dev->d->ctx) c->numLanes = lanes ? lanes : GpuCtx::default_lanes();
   return 0;
   DEV_END(-1)

@@ -269,6 +269,9 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
 
   BvhResult bvh;
   build_bvh(triVerts, triFlags, stackDepth, bvh, anyMotion ? &triVerts1 : nullptr);
+  // each leaf record carries its triangle's geometry id (GpuTri::e2[3]) for the closest-hit
+  // kernels' hitGeom output
+  for (size_t i = 0; i < bvh.tris.size(); ++i) memcpy(&bvh.tris[i].e2[3], &triGeom[bvh.order[i]], 4);
   S->hasMotion = anyMotion;
   S->bvhDepth = bvh.maxDepth;
   S->numTris = gidBase;

@@ -131,7 +131,7 @@ long strtol10(const char* in, const char** out) {
   unsigned long v = 0;  // unsigned: an over-long digit run wraps instead of overflowing (UB)
   while (is_digit(*in)) v = v * 10 + (unsigned long)(*in++ - '0');
   *out = in;
-  return inv ? -(long)v : (long)v;
+  return inv ? (long)(0ul - v) : (long)v;  // negated in unsigned arithmetic: no overflow for v = 2^63
 }
 
 // ---------------------------------------------------------------- XML DOM

@@ -560,6 +560,9 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   // u = U/|den|, v = V/|den| are divided once, when the finished query is stored at the next
   // refill (or at the wave's end), instead of at every accepted hit; q = -1: nothing to store
   float bestDen = 1.f;
+  // closest hit: the accepted triangle's geometry id (GpuTri::e2[3]), stored beside the hit
+  // (occOut) so k_shade loads the geometry record beside the shading record, not after it
+  int bestGeom = 0;
   q = -1;
   // PRIM: a finished camera ray (q = its path id) — a hit is appended with its ray and hit
   // record to the depth-0 queue segment of its path id's 64-group (one atomic per segment among
@@ -587,6 +590,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         pr.qOrg[slot] = ro;
         pr.qDir[slot] = rd;
         hitOut[slot] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
+        occOut[slot] = bestGeom;
       }
       m &= ~sub;
     }
@@ -595,8 +599,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   do {                                                                                               \
     if constexpr (PRIM)                                                                              \
       prim_store();                                                                                  \
-    else                                                                                             \
+    else {                                                                                           \
       hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri)); \
+      if (occOut) occOut[q] = bestGeom;                                                              \
+    }                                                                                                \
     q = -1;                                                                                          \
   } while (0)
 
@@ -838,6 +844,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             const bool ok = g & (t > r.tnear) & ((t < best.t + 0.0f) | tie);
             if (ok & (k < lTake)) {
               best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
+              bestGeom = __float_as_int(tt[k].e2[3]);
             }
           }
         }
@@ -857,6 +864,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             }
             if (ok) {
               best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
+              bestGeom = __float_as_int(tr.e2[3]);
             }
           }
         }
@@ -1402,6 +1410,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     bool ignoreVL = false, unbent = false, isHit = false, useDirect = false;
     bool haveL = false;  // L holds pathL[path] plus this vertex's emission (written back below)
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+    int hg = 0;
     DG dg;
     BRDFSet bs;
     bs.n = 0;
@@ -1418,6 +1427,9 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     if (active) {
       path = pb.qPath[cur][q];
       h = pb.hit[q];
+#ifndef YRT_NO_HIT_GEOM
+      hg = pb.hitGeom[q];
+#endif
       if (depthLevel == 0) {
         // camera rays (k_raygen): throughput 1, depth 0, unbent, vacuum, zero radiance so far;
         // pathL is written below for every queued path
@@ -1490,7 +1502,13 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       const float4 o = pb.qOrg[cur][q];
       org = v3(o.x, o.y, o.z);
       rec = fv.pixelSets[pixelId] * rp.spp + s;
-      g = __float_as_int(r0.w);  // geometry id rides in the shading record
+      // the geometry id comes with the hit (k_trace's hitGeom), so its record is loaded beside
+      // the shading record: hit -> {shading record, geometry record} -> texels
+#ifdef YRT_NO_HIT_GEOM
+      g = __float_as_int(r0.w);  // (A/B: the geometry id of the shading record, one level later)
+#else
+      g = hg;
+#endif
       const GpuGeomRec& gr = sv.geomRecs[g];
       const int mat = gr.g.material;
       // tangents only feed the Obj bump map and the anisotropic microfacet
@@ -1839,21 +1857,23 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
   hipLaunchKernelGGL(k_raygen, dim3(grid_for(pb.capacity, YRT_BLOCK, YRT_RAYGEN_GRID)), dim3(YRT_BLOCK), 0, s, fv, pb, bi);
 }
 
+// closest hit: the kernel's int output (occOut, the any-hit occlusion flags) carries the hit's
+// geometry id
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time) {
+                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time, int* hitGeom) {
   const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   if (time)
     hipLaunchKernelGGL((k_trace<false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
-                       hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, time, PrimaryRays{});
+                       hit, hitGeom, sv.traceSpill, ShadowFuse{}, time, PrimaryRays{});
   else
     hipLaunchKernelGGL((k_trace<false, false>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
-                       segCap, hit, (int*)nullptr, sv.traceSpill, ShadowFuse{}, (const float*)nullptr, PrimaryRays{});
+                       segCap, hit, hitGeom, sv.traceSpill, ShadowFuse{}, (const float*)nullptr, PrimaryRays{});
 }
 
-void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s) {
+void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, int* hitGeom, hipStream_t s) {
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   hipLaunchKernelGGL((k_trace<false, false, 1>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
-                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, (int*)nullptr, sv.traceSpill,
+                     (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, hitGeom, sv.traceSpill,
                      ShadowFuse{}, (const float*)nullptr, pr);
 }
 

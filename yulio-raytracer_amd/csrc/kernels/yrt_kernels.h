@@ -94,6 +94,8 @@ struct PathBuffers {
   float4* qDir[2];   // xyz, tfar
   float4* qThr[2];   // throughput xyz, w = meta bits: depth | ignoreVL<<8 | unbent<<9
   float4* hit;       // t, u, v, tri (bits), per closest-queue slot
+  int* hitGeom;      // the hit triangle's geometry id, per closest-queue slot: k_shade loads its
+                     // geometry record beside the shading record instead of after it
   float4* pathL;     // per path id: radiance so far (emission and unoccluded direct light are
                      // read-modify-written in the reference's order; one writer per path at a time)
   int* shFirst;      // per (queue slot, light): shadow-ray slot or -1
@@ -155,12 +157,14 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 // Every launch gets the full grid for the queue's capacity: the kernels grid-stride over the
 // device-side count and idle waves exit at once.
 // time (moving scenes): per-slot ray time (Ray::time); null: static scene (or time 0)
+// hitGeom (optional): the hit triangle's geometry id per slot
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
-                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time = nullptr);
+                          int numSegs, int segCap, float4* hit, hipStream_t s, const float* time = nullptr,
+                          int* hitGeom = nullptr);
 // depth 0 of a batch: camera rays generated, traced and queued (hits) or resolved (misses) in
 // one kernel, see PrimaryRays; replaces launch_raygen + the depth-0 launch_trace_closest for
 // static scenes without a backplate or direction-dependent environment lights
-void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, hipStream_t s);
+void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, int* hitGeom, hipStream_t s);
 void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts, int numSegs,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse = nullptr,
                       const float* time = nullptr);
