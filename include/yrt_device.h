@@ -190,6 +190,9 @@ YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
 /* Copies the host mirror of the BVH (4-wide nodes: 128 B each, numTriRefs leaf tris: 48 B each). */
 YRT_API int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes, void* tris,
                          size_t trisBytes);
+/* The same tree with the any-hit traversal's 64-byte quantized nodes (node i = node i of
+ * yrtExportBVH; layout yulio-raytracer_amd/csrc/common/yrt_qnode.h): numNodes * 64 bytes. */
+YRT_API int yrtExportQuantizedBVH(YRTDevice dev, YRTHandle scene, void* qnodes, size_t qnodesBytes);
 /* Serializes the committed scene graph + renderer + camera as the oracle's input blob
  * (format: oracle/yrt_oracle.h). Returns the byte count; call with buf=NULL to size. */
 YRT_API int64_t yrtExportFrame(YRTDevice dev, YRTHandle renderer, YRTHandle camera, YRTHandle scene, void* buf,

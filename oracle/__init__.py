@@ -49,6 +49,8 @@ _sig("oracle_render_shard", i32, vp, sz, i32, i32, C.c_float, i32, i32, i32, i32
      C.POINTER(OracleStats))
 _sig("oracle_count_visits", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
      C.POINTER(C.c_double), vp, sz)
+_sig("oracle_count_visits_q", i32, vp, sz, vp, sz, vp, vp, i32, i32, C.POINTER(C.c_double),
+     C.POINTER(C.c_double), vp, sz)
 _sig("oracle_random_ints", None, i32, i32, vp)
 _sig("oracle_sample_table", i32, i32, i32, i32, i32, i32, C.c_char_p, vp, sz)
 _sig("oracle_pixel_sets", None, i32, i32, i32, vp)
@@ -141,17 +143,19 @@ def trace(blob: bytes, org4: np.ndarray, dir4: np.ndarray, any_hit=False):
     return hit
 
 
-def count_visits(nodes: np.ndarray, tris: np.ndarray, org4, dir4, any_hit=False, tri_bytes=48):
+def count_visits(nodes: np.ndarray, tris: np.ndarray, org4, dir4, any_hit=False, tri_bytes=48, qnodes=None):
     """Node / triangle visits of the device traversal order over an exported BVH (tri_bytes:
-    the scene's triRecordBytes)."""
+    the scene's triRecordBytes); qnodes: traverse the quantized nodes (Device.export_qbvh)
+    instead of the float ones."""
     org4 = np.ascontiguousarray(org4, np.float32)
     dir4 = np.ascontiguousarray(dir4, np.float32)
     n = org4.shape[0]
     nv, tv = C.c_double(), C.c_double()
     hit = np.zeros((n, 4), np.float32)
-    rc = _lib.oracle_count_visits(nodes.ctypes.data, nodes.nbytes // 128, tris.ctypes.data, tris.nbytes // tri_bytes,
-                                  org4.ctypes.data, dir4.ctypes.data, n, int(any_hit), C.byref(nv), C.byref(tv),
-                                  hit.ctypes.data, tri_bytes)
+    fn, nd, nb = (_lib.oracle_count_visits, nodes, 128) if qnodes is None else (_lib.oracle_count_visits_q, qnodes, 64)
+    rc = fn(nd.ctypes.data, nd.nbytes // nb, tris.ctypes.data, tris.nbytes // tri_bytes,
+            org4.ctypes.data, dir4.ctypes.data, n, int(any_hit), C.byref(nv), C.byref(tv),
+            hit.ctypes.data, tri_bytes)
     if rc != 0:
         raise RuntimeError(f"oracle_count_visits: {_err()}")
     return nv.value, tv.value, hit

@@ -2621,12 +2621,33 @@ int oracle_scene_triangles(const void* blob, size_t bytes, float* out, int maxTr
  * these counts are a lower bound on the kernel's node fetches. */
 typedef struct { float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4]; int32_t child[4], pad[4]; } DNode;
 typedef struct { float v0[4], e1[4], e2[4]; } DTri;
+/* The 64-B quantized node of the same index (yulio-raytracer_amd/csrc/common/yrt_qnode.h): origin,
+ * biased quantum exponents, children, plane bytes (lo x, hi x, lo y, hi y, lo z, hi z; byte k =
+ * child k). The kernel's box4_quant: per axis a = fma(origin, inv, -org*inv) and
+ * s = 2^e * inv, per plane fma(q, s, a). */
+typedef struct { float origin[3]; uint32_t exps; int32_t child[4]; uint32_t q[6], pad[2]; } QNode;
+static int count_visits_impl(const void* nodes_, const void* qnodes_, const void* tris_, const float* org4,
+                             const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
+                             size_t triStride);
 int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, size_t numTris, const float* org4,
                         const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
                         size_t triStride /* bytes per leaf record: 48, or 64 with a stored normal */) {
-  const DNode* nodes = (const DNode*)nodes_;
-  const char* trisBytes = (const char*)tris_;
   (void)numNodes; (void)numTris;
+  return count_visits_impl(nodes_, NULL, tris_, org4, dir4, n, anyHit, nodeVisits, triVisits, hit4, triStride);
+}
+/* the same traversal on the quantized nodes (the any-hit kernel's) */
+int oracle_count_visits_q(const void* qnodes_, size_t numNodes, const void* tris_, size_t numTris, const float* org4,
+                          const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
+                          size_t triStride) {
+  (void)numNodes; (void)numTris;
+  return count_visits_impl(NULL, qnodes_, tris_, org4, dir4, n, anyHit, nodeVisits, triVisits, hit4, triStride);
+}
+static int count_visits_impl(const void* nodes_, const void* qnodes_, const void* tris_, const float* org4,
+                             const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
+                             size_t triStride) {
+  const DNode* nodes = (const DNode*)nodes_;
+  const QNode* qnodes = (const QNode*)qnodes_;
+  const char* trisBytes = (const char*)tris_;
   double nv = 0, tv = 0;
   const float INF = (float)INFINITY;
   for (int i = 0; i < n; ++i) {
@@ -2643,19 +2664,34 @@ int oracle_count_visits(const void* nodes_, size_t numNodes, const void* tris_, 
       int stack[128], sp = 0, cur = 0, done = 0;
       while (!done) {
         if ((cur & 31) == 0) {
-          const DNode* nd = &nodes[cur >> 5];
           nv += 1;
           float t[4];
           int c[4];
           for (int k = 0; k < 4; ++k) {
-            const float lo[3] = {nd->lox[k], nd->loy[k], nd->loz[k]}, hi[3] = {nd->hix[k], nd->hiy[k], nd->hiz[k]};
             float l[3], h[3];
-            for (int a = 0; a < 3; ++a) { l[a] = fmaf(lo[a], iv[a], -oi[a]); h[a] = fmaf(hi[a], iv[a], -oi[a]); }
+            int child;
+            if (qnodes) {
+              const QNode* qn = &qnodes[cur >> 5];
+              for (int a = 0; a < 3; ++a) {
+                uint32_t eb = ((qn->exps >> (8 * a)) & 0xffu) << 23;
+                float scale;
+                memcpy(&scale, &eb, 4);
+                const float s = scale * iv[a], ax = fmaf(qn->origin[a], iv[a], -oi[a]);
+                l[a] = fmaf((float)((qn->q[2 * a] >> (8 * k)) & 0xffu), s, ax);
+                h[a] = fmaf((float)((qn->q[2 * a + 1] >> (8 * k)) & 0xffu), s, ax);
+              }
+              child = qn->child[k];
+            } else {
+              const DNode* nd = &nodes[cur >> 5];
+              const float lo[3] = {nd->lox[k], nd->loy[k], nd->loz[k]}, hi[3] = {nd->hix[k], nd->hiy[k], nd->hiz[k]};
+              for (int a = 0; a < 3; ++a) { l[a] = fmaf(lo[a], iv[a], -oi[a]); h[a] = fmaf(hi[a], iv[a], -oi[a]); }
+              child = nd->child[k];
+            }
             const float nn = fmaxf(fmaxf(fminf(l[0], h[0]), fminf(l[1], h[1])), fmaxf(fminf(l[2], h[2]), r.tnear));
             const float ff = fminf(fminf(fmaxf(l[0], h[0]), fmaxf(l[1], h[1])), fminf(fmaxf(l[2], h[2]), best.t));
-            const int hit = nn <= fmaf(ff, 1.0000152587890625f, margin) && nd->child[k] != -1;
+            const int hit = nn <= fmaf(ff, 1.0000152587890625f, margin) && child != -1;
             t[k] = hit ? nn : INF;
-            c[k] = nd->child[k];
+            c[k] = child;
           }
           /* 5-comparator sort network, as the kernel's sort4; any-hit rays take the farthest
            * hit child first, the others in slot order (the kernel's sort3_far: descending

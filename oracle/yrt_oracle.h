@@ -83,6 +83,10 @@ int oracle_count_visits(const void* nodes, size_t numNodes, const void* tris, si
                         const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits,
                         float* hit4,
                         size_t triStride);
+/* the same traversal on the 64-B quantized nodes (common/yrt_qnode.h) of the same tree */
+int oracle_count_visits_q(const void* qnodes, size_t numNodes, const void* tris, size_t numTris, const float* org4,
+                          const float* dir4, int n, int anyHit, double* nodeVisits, double* triVisits, float* hit4,
+                          size_t triStride);
 
 /* Reference Random (common/math/random.h): n draws of getInt() after setSeed(seed). */
 void oracle_random_ints(int seed, int n, int32_t* out);

@@ -159,6 +159,81 @@ def test_device_bvh_gives_oracle_hits(host_device, which, sbvh, monkeypatch):
     s.close()
 
 
+def _qnode_planes(q):
+    """Dequantized planes of exported quantized nodes, exactly (float64): origin + q * 2^e."""
+    rec = q.reshape(-1, 64)
+    origin = rec[:, 0:12].copy().view(np.float32).astype(np.float64)          # (n, 3)
+    exps = rec[:, 12:16].copy().view(np.uint32)[:, 0]
+    child = rec[:, 16:32].copy().view(np.int32)                                # (n, 4)
+    words = rec[:, 32:56].copy().view(np.uint32)                               # (n, 6)
+    scale = np.stack([2.0 ** (((exps >> (8 * a)) & 0xFF).astype(np.int64) - 127) for a in range(3)], 1)
+    byte = (words[:, :, None] >> (8 * np.arange(4))[None, None, :]) & 0xFF      # (n, 6, 4)
+    lo = origin[:, :, None] + byte[:, 0::2, :] * scale[:, :, None]              # (n, 3, 4)
+    hi = origin[:, :, None] + byte[:, 1::2, :] * scale[:, :, None]
+    return lo, hi, scale, child
+
+
+@pytest.mark.parametrize("which", ["C2", "C3", "C4", "C5"])
+def test_quantized_nodes_contain_the_float_boxes(host_device, which):
+    """The any-hit kernel's 64-B nodes (common/yrt_qnode.h): node for node the same children,
+    and every dequantized child box contains the float node's child box widened by one quantum
+    on every side (the slack that keeps the kernel's box test conservative)."""
+    if which == "C5":
+        from yrt import frederick
+        dae = frederick.write_dae()
+        s = yrt.Session(["-fprCollada", "-i", str(dae), "-stereo", "-size", "32", "32", "-spp", "1"],
+                        device=host_device)
+    else:
+        s = yrt.Session({"C2": c2_args(32, 1), "C3": c3_args(32, 1), "C4": c4_args(32, 1)}[which], device=host_device)
+    scene = s.info()["scene"]
+    nodes, _ = host_device.export_bvh(scene)
+    q = host_device.export_qbvh(scene)
+    nd = nodes.reshape(-1, 128)
+    planes = nd[:, :96].copy().view(np.float32).reshape(-1, 6, 4).astype(np.float64)  # lox hix loy hiy loz hiz
+    fchild = nd[:, 96:112].copy().view(np.int32)
+    lo, hi, scale, qchild = _qnode_planes(q)
+    assert np.array_equal(fchild, qchild)
+    valid = fchild != -1
+    for a in range(3):
+        s_ = scale[:, a][:, None]
+        assert np.all((lo[:, a, :] <= planes[:, 2 * a, :] - s_) | ~valid)
+        assert np.all((hi[:, a, :] >= planes[:, 2 * a + 1, :] + s_) | ~valid)
+    # the quantum is a small fraction of the node: at most 1/250 of its extent, or 2 float ulps
+    v3 = valid[:, None, :]
+    L = np.where(v3, planes[:, 0::2, :], np.inf).min(2)
+    H = np.where(v3, planes[:, 1::2, :], -np.inf).max(2)
+    ok = valid.any(1)
+    E = (H - L)[ok]
+    m = np.maximum(np.abs(L), np.abs(H))[ok]
+    assert np.all(scale[ok] <= np.maximum(E / 125.0, 2.0 ** -100) + 4 * m * 2.0 ** -23)
+    s.close()
+
+
+@pytest.mark.parametrize("which", ["C2", "C3"])
+def test_quantized_nodes_give_the_same_hits(host_device, which):
+    """Closest hits and occlusion of 4096 incoherent rays through the quantized nodes, in the
+    kernel's traversal order, equal the float nodes' (and so the oracle's own BVH's)."""
+    s = yrt.Session({"C2": c2_args(32, 1), "C3": c3_args(32, 1)}[which], device=host_device)
+    scene = s.info()["scene"]
+    blob = s.export_frame()
+    nodes, tris = host_device.export_bvh(scene)
+    q = host_device.export_qbvh(scene)
+    tb = host_device.scene_info(scene)["triRecordBytes"]
+    org4, dir4 = _incoherent(blob, 4096)
+    for any_hit in (False, True):
+        d = dir4.copy()
+        if any_hit:
+            d[::2, 3] = 50.0
+        nv, tv, h = oracle.count_visits(nodes, tris, org4, d, any_hit=any_hit, tri_bytes=tb)
+        nq, tq, hq = oracle.count_visits(nodes, tris, org4, d, any_hit=any_hit, tri_bytes=tb, qnodes=q)
+        if any_hit:
+            assert np.array_equal(h[:, 3].view(np.int32) >= 0, hq[:, 3].view(np.int32) >= 0)
+        else:
+            assert np.array_equal(h.view(np.uint32), hq.view(np.uint32))
+        assert nv <= nq < 1.5 * nv, (nv, nq)
+    s.close()
+
+
 def test_bvh_depth_within_stack(host_device):
     s = yrt.Session(c3_args(32, 1), device=host_device)
     info = host_device.scene_info(s.info()["scene"])

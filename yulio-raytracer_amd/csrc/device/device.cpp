@@ -1896,6 +1896,17 @@ int yrtExportBVH(YRTDevice dev, YRTHandle scene, void* nodes, size_t nodesBytes,
   return 0;
   DEV_END(-1)
 }
+int yrtExportQuantizedBVH(YRTDevice dev, YRTHandle scene, void* qnodes, size_t qnodesBytes) {
+  DEV_GUARD(dev, -1)
+  auto S = dev->d->get<SceneObj>(scene, "scene");
+  if (!S->gpu) throw std::runtime_error("scene not committed");
+  sync_host_bvh(*S->gpu);
+  const size_t nb = S->gpu->hQNodes.size() * sizeof(GpuQNode);
+  if (qnodesBytes < nb) throw std::runtime_error("buffer too small");
+  memcpy(qnodes, S->gpu->hQNodes.data(), nb);
+  return 0;
+  DEV_END(-1)
+}
 int yrtSetFrameSeed(YRTDevice dev, uint32_t seed) {
   DEV_GUARD(dev, -1)
   dev->d->frameSeed = seed;

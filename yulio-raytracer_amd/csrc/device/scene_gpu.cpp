@@ -20,6 +20,7 @@ namespace yrt {
 static void bind_view(GpuScene& S) {
   SceneView& v = S.view;
   v.nodes = S.nodes.as<GpuNode>();
+  v.qnodes = S.qnodes.as<GpuQNode>();
   v.tris = S.tris.as<GpuTri>();
   v.triGeom = S.triGeom.as<int>();
   v.indices = S.indices.as<int4>();
@@ -272,6 +273,9 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   // each leaf record carries its triangle's geometry id (GpuTri::e2[3]) for the closest-hit
   // kernels' hitGeom output
   for (size_t i = 0; i < bvh.tris.size(); ++i) memcpy(&bvh.tris[i].e2[3], &triGeom[bvh.order[i]], 4);
+  // the any-hit kernels' 64-B nodes (common/yrt_qnode.h), node for node
+  std::vector<GpuQNode> qnodes(bvh.nodes.size());
+  for (size_t i = 0; i < bvh.nodes.size(); ++i) yrt_quantize_node(bvh.nodes[i], qnodes[i]);
   S->hasMotion = anyMotion;
   S->bvhDepth = bvh.maxDepth;
   S->numTris = gidBase;
@@ -285,6 +289,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
 
   if (!upload) {
     S->hNodes = std::move(bvh.nodes);
+    S->hQNodes = std::move(qnodes);
     S->hTris = std::move(bvh.tris);
     S->hGeoms = geoms;
     S->hTriGeom = triGeom;
@@ -305,6 +310,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   for (const GpuMaterial& m : materials) S->materialMask |= 1u << m.type;
   for (const GpuLight& l : lights) S->materialMask |= 1u << (16 + l.type);  // light_bit (kernels/yrt_shade.h)
   S->nodes.upload(bvh.nodes);
+  S->qnodes.upload(qnodes);
   S->tris.upload(bvh.tris);
   S->triGeom.upload(triGeom);
   S->indices.upload(indices);
@@ -445,6 +451,7 @@ std::shared_ptr<GpuScene> build_gpu_scene(const std::vector<std::shared_ptr<Scen
   }
 
   S->hNodes = std::move(bvh.nodes);
+  S->hQNodes = std::move(qnodes);
   S->hTris = std::move(bvh.tris);
   S->hGeoms = geoms;
   S->hTriGeom = triGeom;
@@ -463,6 +470,7 @@ std::shared_ptr<GpuScene> replicate_gpu_scene(const GpuScene& src, int device) {
     HIP_CHECK(hipMemcpyPeer(dst.p, device, from.p, src.device, from.bytes));
   };
   copy(R->nodes, src.nodes);
+  copy(R->qnodes, src.qnodes);
   copy(R->tris, src.tris);
   copy(R->triGeom, src.triGeom);
   copy(R->indices, src.indices);
@@ -548,6 +556,7 @@ bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>&
   for (int d = (int)S.levelStart.size() - 2; d >= 0; --d)
     launch_refit_nodes(S.nodes.as<GpuNode>(), S.tris.as<GpuTri>(), S.indices.as<int4>(), S.positions.as<float4>(),
                        S.levelNodes.as<int>() + S.levelStart[d], S.levelStart[d + 1] - S.levelStart[d], stream);
+  launch_quantize_nodes(S.nodes.as<GpuNode>(), S.qnodes.as<GpuQNode>(), (int)S.hNodes.size(), stream);
   HIP_CHECK(hipStreamSynchronize(stream));
   S.hostBvhStale = true;
   S.refits++;
@@ -558,6 +567,7 @@ bool refit_gpu_scene(GpuScene& S, const std::vector<std::shared_ptr<ScenePrim>>&
 void sync_host_bvh(GpuScene& S) {
   if (!S.hostBvhStale) return;
   HIP_CHECK(hipMemcpy(S.hNodes.data(), S.nodes.p, S.hNodes.size() * sizeof(GpuNode), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(S.hQNodes.data(), S.qnodes.p, S.hQNodes.size() * sizeof(GpuQNode), hipMemcpyDeviceToHost));
   HIP_CHECK(hipMemcpy(S.hTris.data(), S.tris.p, S.hTris.size() * sizeof(GpuTri), hipMemcpyDeviceToHost));
   S.hostBvhStale = false;
 }

@@ -58,7 +58,7 @@ struct GpuScene {
     static std::atomic<uint64_t> n{1};
     return n++;
   }
-  DevBuf nodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
+  DevBuf nodes, qnodes, tris, triGeom, indices, positions, normals, texcoords, geoms, materials, textures, images, texels, texQuads,
       lights, envLights, hdriDist, media, geomRecs, motions, tangents, triMotion, triShade;
   bool hasMotion = false;  // moving geometry: time-aware trace kernels, no refit
   SceneView view{};
@@ -66,6 +66,7 @@ struct GpuScene {
   size_t texels8Bytes = 0;    // the 8-bit images' part of the texel pool (float images follow it)
   // host mirrors (BVH export, precomputed light sampling, stats)
   std::vector<GpuNode> hNodes;
+  std::vector<GpuQNode> hQNodes;  // the same tree with 64-B quantized nodes (common/yrt_qnode.h)
   std::vector<GpuTri> hTris;
   std::vector<GpuGeom> hGeoms;
   std::vector<int> hTriGeom;

@@ -418,6 +418,14 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
+// Node format per traversal kind: 1 = the 64-B quantized nodes (common/yrt_qnode.h), 0 = the
+// 128-B float nodes. Both give the same query results bit for bit (conservative boxes).
+#ifndef YRT_QNODES_ANY
+#define YRT_QNODES_ANY 1
+#endif
+#ifndef YRT_QNODES_CLOSEST
+#define YRT_QNODES_CLOSEST 0
+#endif
 #ifndef YRT_NODE_BIAS_ANY
 #define YRT_NODE_BIAS_ANY 20  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %;
                               // four lanes (r05gg-ii): 24 / 32 C3 -2.0 / -2.8 % but C5 +1.6 / +2.3 %
@@ -511,6 +519,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   if (next >= end) return;  // wave-uniform
 
   const GpuNode* __restrict__ nodes = sv.nodes;
+  const GpuQNode* __restrict__ qnodes = sv.qnodes;
   const GpuTri* __restrict__ tris = sv.tris;
   int* stack = lstack + threadIdx.x;
   // Deep stack entries (rare) spill to global memory, [entry][thread]: a private array here
@@ -755,7 +764,10 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         float t[4];
         int c[4];
         // sign-ordered slab planes (+1.5 % on C3 with two lanes, bit-identical distances)
-        box4_ordered<ANY>(r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
+        if (ANY ? YRT_QNODES_ANY : YRT_QNODES_CLOSEST)
+          box4_quant<ANY>(r, __float_as_int(ri.w), best.t, t, c, qnodes, curIdx);
+        else
+          box4_ordered<ANY>(r, __float_as_int(ri.w), best.t, t, c, nodes, curIdx);
         // closest-hit rays sort the hit children by entry distance (nearest next, the others
         // pushed farthest-first); any-hit rays take the farthest hit child next and push the
         // others in slot order (sort3_far: -22 % node visits against slot order)
@@ -2263,6 +2275,21 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_refit_nodes(GpuNode* __restrict__
     n.loy[k] = lo[1]; n.hiy[k] = hi[1];
     n.loz[k] = lo[2]; n.hiz[k] = hi[2];
   }
+}
+
+__global__ __launch_bounds__(YRT_BLOCK) void k_quantize_nodes(const GpuNode* __restrict__ nodes,
+                                                             GpuQNode* __restrict__ qnodes, int count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  GpuQNode q;
+  yrt_quantize_node(nodes[i], q);  // the host builder's function: the same bytes
+  qnodes[i] = q;
+}
+
+void launch_quantize_nodes(const GpuNode* nodes, GpuQNode* qnodes, int count, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(k_quantize_nodes, dim3((count + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes, qnodes,
+                     count);
 }
 
 void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices, const float4* positions,

@@ -6,12 +6,14 @@
 #include <stdint.h>
 
 #include "../common/yrt_gpu_types.h"
+#include "../common/yrt_qnode.h"
 #include "yrt_traverse.h"
 
 namespace yrt {
 
 struct SceneView {
   const GpuNode* nodes;
+  const GpuQNode* qnodes;  // the same tree, 64-B quantized nodes (any-hit traversal)
   const GpuTri* tris;
   const int* triGeom;
   const int4* indices;
@@ -207,6 +209,8 @@ void launch_refit_tris(GpuTri* tris, GpuTriShade* triShade, const int4* indices,
                        hipStream_t s);
 void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices, const float4* positions,
                         const int* levelNodes, int count, hipStream_t s);
+// the quantized copy of every node (yrt_quantize_node), after a refit of the float nodes
+void launch_quantize_nodes(const GpuNode* nodes, GpuQNode* qnodes, int count, hipStream_t s);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 

@@ -21,6 +21,7 @@
 
 #include "../common/yrt_gpu_types.h"
 #include "../common/yrt_math.h"
+#include "../common/yrt_qnode.h"
 
 #ifndef YRT_STACK_DEPTH
 #define YRT_STACK_DEPTH 64   // bound on traversal stack entries + 1 (device/bvh_build.cpp enforces it)
@@ -185,6 +186,62 @@ __device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, fl
     asm("v_min_f32 %0, %1, %2" : "=v"(b_) : "v"(FZ), "v"(tmax));                            \
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(ff) : "v"(FX), "v"(FY), "v"(b_));                \
     t[k] = nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin) ? nn : MISS;                  \
+    c[k] = (CH);                                                                            \
+  } while (0)
+  YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
+  YRT_CHILD(1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y, ch.y);
+  YRT_CHILD(2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x, ch.z);
+  YRT_CHILD(3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y, ch.w);
+#undef YRT_CHILD
+}
+
+// box4_ordered on the 64-B quantized node of the same index (common/yrt_qnode.h): one 64-B line
+// (four loads: origin + quantum exponents, children, lo/hi words of x and y, of z) instead of
+// seven 16-B loads from 128 B. Per axis a = fma(origin, inv, -org * inv) and s = 2^e * inv
+// (exact); per plane one v_cvt_f32_ubyte and one FMA (packed two children at a time), the near
+// and far words picked by the ray's direction signs (planeOff, as box4_ordered). The planes lie
+// at least one quantum outside the float node's child boxes, which covers a's rounding (see
+// yrt_qnode.h), so the same boxes are never culled and every query returns the same bits.
+// Empty slots are tested by their child reference.
+template <bool ANY>
+__device__ __forceinline__ void box4_quant(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
+                                           const GpuQNode* __restrict__ base, int nodeIdx) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const char* b0 = (const char*)base + ((unsigned)nodeIdx << 6);
+  const float4 h = *(const float4*)b0;
+  const int4 ch = *(const int4*)(b0 + 16);
+  const uint4 pa = *(const uint4*)(b0 + 32);   // lo x, hi x, lo y, hi y
+  const uint2 pb = *(const uint2*)(b0 + 48);   // lo z, hi z
+  const uint32_t ex = __float_as_uint(h.w);
+  const float sx = __uint_as_float((ex & 0xffu) << 23) * r.inv.x;
+  const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23) * r.inv.y;
+  const float sz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * r.inv.z;
+  const float ax = __builtin_fmaf(h.x, r.inv.x, -r.oi.x);
+  const float ay = __builtin_fmaf(h.y, r.inv.y, -r.oi.y);
+  const float az = __builtin_fmaf(h.z, r.inv.z, -r.oi.z);
+  const bool hx = (planeOff & 16) != 0, hy = (planeOff & (16 << 8)) != 0, hz = (planeOff & (16 << 16)) != 0;
+  const uint32_t nwx = hx ? pa.y : pa.x, fwx = hx ? pa.x : pa.y;
+  const uint32_t nwy = hy ? pa.w : pa.z, fwy = hy ? pa.z : pa.w;
+  const uint32_t nwz = hz ? pb.y : pb.x, fwz = hz ? pb.x : pb.y;
+#define YRT_QB(w, k) ((float)(((w) >> (8 * (k))) & 0xffu))
+#define YRT_QSLAB(W, S, A, k0, k1) __builtin_elementwise_fma((f2{YRT_QB(W, k0), YRT_QB(W, k1)}), (f2{S, S}), (f2{A, A}))
+  const f2 nx01 = YRT_QSLAB(nwx, sx, ax, 0, 1), nx23 = YRT_QSLAB(nwx, sx, ax, 2, 3);
+  const f2 fx01 = YRT_QSLAB(fwx, sx, ax, 0, 1), fx23 = YRT_QSLAB(fwx, sx, ax, 2, 3);
+  const f2 ny01 = YRT_QSLAB(nwy, sy, ay, 0, 1), ny23 = YRT_QSLAB(nwy, sy, ay, 2, 3);
+  const f2 fy01 = YRT_QSLAB(fwy, sy, ay, 0, 1), fy23 = YRT_QSLAB(fwy, sy, ay, 2, 3);
+  const f2 nz01 = YRT_QSLAB(nwz, sz, az, 0, 1), nz23 = YRT_QSLAB(nwz, sz, az, 2, 3);
+  const f2 fz01 = YRT_QSLAB(fwz, sz, az, 0, 1), fz23 = YRT_QSLAB(fwz, sz, az, 2, 3);
+#undef YRT_QSLAB
+#undef YRT_QB
+  const float MISS = __int_as_float(ANY ? 0xff800000 : 0x7f800000);
+#define YRT_CHILD(k, NX, FX, NY, FY, NZ, FZ, CH)                                            \
+  do {                                                                                      \
+    float nn, ff, a_, b_;                                                                   \
+    asm("v_max_f32 %0, %1, %2" : "=v"(a_) : "v"(NZ), "v"(r.tnear));                         \
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(nn) : "v"(NX), "v"(NY), "v"(a_));                \
+    asm("v_min_f32 %0, %1, %2" : "=v"(b_) : "v"(FZ), "v"(tmax));                            \
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(ff) : "v"(FX), "v"(FY), "v"(b_));                \
+    t[k] = (nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin)) & ((CH) != -1) ? nn : MISS; \
     c[k] = (CH);                                                                            \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);

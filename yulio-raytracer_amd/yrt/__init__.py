@@ -325,6 +325,13 @@ class Device:
                  "export_bvh")
         return nodes, tris
 
+    def export_qbvh(self, scene):
+        """The any-hit traversal's quantized nodes (uint8[numNodes*64], common/yrt_qnode.h)."""
+        info = self.scene_info(scene)
+        q = np.zeros(info["numNodes"] * 64, np.uint8)
+        self._rc(N.dev.yrtExportQuantizedBVH(self.h, scene, q.ctypes.data, q.nbytes), "export_qbvh")
+        return q
+
     def export_frame(self, renderer, camera, scene) -> bytes:
         n = N.dev.yrtExportFrame(self.h, renderer, camera, scene, None, 0)
         if n < 0:
