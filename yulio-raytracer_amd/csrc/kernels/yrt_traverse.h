@@ -241,7 +241,7 @@ __device__ __forceinline__ void box4_quant(const RayPre& r, int planeOff, float 
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(nn) : "v"(NX), "v"(NY), "v"(a_));                \
     asm("v_min_f32 %0, %1, %2" : "=v"(b_) : "v"(FZ), "v"(tmax));                            \
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(ff) : "v"(FX), "v"(FY), "v"(b_));                \
-    t[k] = (nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin)) & ((CH) != -1) ? nn : MISS; \
+    t[k] = ((int)(nn <= __builtin_fmaf(ff, YRT_BOX_ROBUST, r.margin)) & (int)((CH) != -1)) ? nn : MISS; \
     c[k] = (CH);                                                                            \
   } while (0)
   YRT_CHILD(0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x, ch.x);
