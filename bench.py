@@ -35,7 +35,8 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md §HBM
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md §L2 (per XCD, 32 MiB aggregate): ≈34.5 TB/s
-NODE_BYTES = 128  # GpuNode (4-wide); triangle record bytes from the scene (GpuTri, 48 or 64)
+# node and triangle record bytes come from the scene (YRTSceneInfo nodeBytesClosest / nodeBytesAny:
+# 128-B float nodes or 64-B quantized ones; triRecordBytes: GpuTri, 48)
 
 
 def parse():
@@ -215,8 +216,12 @@ def main():
         avg_ms_overlapped = ms / max(nl, 1)
         avg_ms = avg_ms_overlapped
         if serial:
-            sk = {"closest": ("msTraceClosest", "launchesClosest"), "shadow": ("msTraceShadow", "launchesShadow")}[dom]
+            # the one-lane frame's own launches, queries and time (its batches may be split
+            # differently from the timed frames': ADVICE r5)
+            sk = {"closest": ("msTraceClosest", "launchesClosest", "raysClosest"),
+                  "shadow": ("msTraceShadow", "launchesShadow", "raysShadow")}[dom]
             avg_ms = serial[sk[0]] / max(serial[sk[1]], 1)
+            nr, nl = serial[sk[2]], serial[sk[1]]
         kname = "k_trace<false>" if dom == "closest" else "k_trace<true>"
         alg = nr * per_kind[dom]["bytes_per_ray"] / max(nl, 1) if per_kind else None
         alg_gbs = alg / (avg_ms * 1e-3) / 1e9 if alg and avg_ms > 0 else None
@@ -247,7 +252,8 @@ def main():
                 "algorithmic_hbm_frac": round(alg_gbs / HBM_PEAK_GBS, 4) if alg_gbs else None,
                 "l2_frac": round(alg_gbs / L2_PEAK_GBS, 4) if alg_gbs else None,
                 "l2_peak_gbs": L2_PEAK_GBS,
-                "algorithmic_note": "SURVEY 8(d) bytes (ray+hit+N_node*128+N_tri*48); node/triangle reads are "
+                "algorithmic_note": "SURVEY 8(d) bytes (ray+hit+N_node*node_bytes+N_tri*48, node_bytes 128 float "
+                                    "or 64 quantized); node/triangle reads are "
                                     "L2/MALL hits (counter HBM traffic is 'hbm'), so algorithmic_hbm_frac can exceed "
                                     "1; l2_frac is the same bytes against the L2 peak",
                 "pmc_source": pmc_note,
@@ -357,14 +363,19 @@ def visit_counts(a, dev, R, cam, S, T, F, sinfo):
     dev.rtRenderFrame(R, cam, S, T, F, 0)
     dev.set_ray_capture(0)
     nodes, tris = dev.export_bvh(S)
+    qnodes = dev.export_qbvh(S)
     per_kind = {}
     for shadow in (0, 1):
+        # the node format the kernel traverses: 64-B quantized nodes (any-hit by default) or the
+        # 128-B float ones; the oracle counts visits on the same records
+        nb = sinfo["nodeBytesAny" if shadow else "nodeBytesClosest"]
         tot_rays = tot_nodes = tot_tris = 0.0
         for depth in range(64):
             org, dr, total = dev.captured_rays(shadow, depth)
             if len(org):
                 nv, tv, _ = oracle.count_visits(nodes, tris, org, dr, any_hit=bool(shadow),
-                                                tri_bytes=sinfo["triRecordBytes"])
+                                                tri_bytes=sinfo["triRecordBytes"],
+                                                qnodes=qnodes if nb == 64 else None)
                 tot_rays += total
                 tot_nodes += nv / len(org) * total
                 tot_tris += tv / len(org) * total
@@ -372,8 +383,8 @@ def visit_counts(a, dev, R, cam, S, T, F, sinfo):
         n_tri = tot_tris / max(tot_rays, 1)
         io = 32 + (4 if shadow else 16)
         per_kind["shadow" if shadow else "closest"] = {
-            "nodes_per_ray": n_node, "tris_per_ray": n_tri,
-            "bytes_per_ray": io + n_node * NODE_BYTES + n_tri * sinfo["triRecordBytes"]}
+            "nodes_per_ray": n_node, "tris_per_ray": n_tri, "node_bytes": nb,
+            "bytes_per_ray": io + n_node * nb + n_tri * sinfo["triRecordBytes"]}
     return per_kind
 
 

@@ -185,6 +185,9 @@ typedef struct YRTSceneInfo {
   float bboxLo[3], bboxHi[3];
   int64_t numTriRefs;
   int64_t triRecordBytes;  /* bytes per leaf triangle record (48, or 64 with a stored normal) */
+  /* bytes per BVH node the closest-hit / any-hit traversal reads: 128 (float planes) or 64
+   * (8-bit quantized planes, yulio-raytracer_amd/csrc/common/yrt_qnode.h) */
+  int64_t nodeBytesClosest, nodeBytesAny;
 } YRTSceneInfo;
 YRT_API int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out);
 /* Copies the host mirror of the BVH (4-wide nodes: 128 B each, numTriRefs leaf tris: 48 B each). */

@@ -1877,6 +1877,8 @@ int yrtGetSceneInfo(YRTDevice dev, YRTHandle scene, YRTSceneInfo* out) {
   out->numNodes = (int64_t)S->gpu->hNodes.size();
   out->numTriRefs = (int64_t)S->gpu->hTris.size();
   out->triRecordBytes = (int64_t)sizeof(GpuTri);
+  out->nodeBytesClosest = trace_node_bytes(false);
+  out->nodeBytesAny = trace_node_bytes(true);
   out->bvhDepth = S->gpu->bvhDepth;
   out->numLights = S->gpu->view.numLights;
   out->buildSeconds = S->gpu->buildSeconds;

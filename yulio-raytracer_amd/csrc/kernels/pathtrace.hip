@@ -2286,6 +2286,10 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_quantize_nodes(const GpuNode* __r
   qnodes[i] = q;
 }
 
+int trace_node_bytes(bool anyHit) {
+  return (anyHit ? YRT_QNODES_ANY : YRT_QNODES_CLOSEST) ? (int)sizeof(GpuQNode) : (int)sizeof(GpuNode);
+}
+
 void launch_quantize_nodes(const GpuNode* nodes, GpuQNode* qnodes, int count, hipStream_t s) {
   if (count <= 0) return;
   hipLaunchKernelGGL(k_quantize_nodes, dim3((count + YRT_BLOCK - 1) / YRT_BLOCK), dim3(YRT_BLOCK), 0, s, nodes, qnodes,

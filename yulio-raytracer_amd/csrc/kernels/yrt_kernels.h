@@ -211,6 +211,8 @@ void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices,
                         const int* levelNodes, int count, hipStream_t s);
 // the quantized copy of every node (yrt_quantize_node), after a refit of the float nodes
 void launch_quantize_nodes(const GpuNode* nodes, GpuQNode* qnodes, int count, hipStream_t s);
+// bytes per node of the closest-hit / any-hit traversal as built (YRT_QNODES_CLOSEST / _ANY)
+int trace_node_bytes(bool anyHit);
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 

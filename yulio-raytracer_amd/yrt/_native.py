@@ -53,7 +53,7 @@ class SceneInfo(C.Structure):
     _fields_ = [("numTriangles", C.c_int64), ("numGeometries", C.c_int64), ("numNodes", C.c_int64),
                 ("bvhDepth", C.c_int64), ("numLights", C.c_int64), ("buildSeconds", C.c_double),
                 ("bboxLo", C.c_float * 3), ("bboxHi", C.c_float * 3), ("numTriRefs", C.c_int64),
-                ("triRecordBytes", C.c_int64)]
+                ("triRecordBytes", C.c_int64), ("nodeBytesClosest", C.c_int64), ("nodeBytesAny", C.c_int64)]
 
 
 class SessionInfo(C.Structure):
