@@ -40,7 +40,6 @@ YRT_HD V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 YRT_HD V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 YRT_HD V3 operator*(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 YRT_HD V3 operator/(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
-YRT_HD V3 rcpv(V3 a) { return v3(1.0f / a.x, 1.0f / a.y, 1.0f / a.z); }
 YRT_HD bool operator==(V3 a, V3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 YRT_HD bool operator!=(V3 a, V3 b) { return !(a == b); }
 // dot, cross and LinearSpace3 * v in the reference build's operation sequences (x64 MSVC, SSE4.1
@@ -92,6 +91,8 @@ YRT_HD float rsqrtf_(float x) { return 1.0f / sqrtf(x); }
 YRT_HD float rcpf_(float x) { return yrt_ref_rcp(x); }    // common/math/math.h:38-42
 YRT_HD float rsqrtf_(float x) { return yrt_ref_rsqrt(x); }  // common/math/math.h:53-58
 #endif
+// rcp of a Color / Vector3f: the same sequence per lane (color_sse.h:142-145, vector3f_sse.h:135-138)
+YRT_HD V3 rcpv(V3 a) { return v3(rcpf_(a.x), rcpf_(a.y), rcpf_(a.z)); }
 YRT_HD V3 normalize(V3 a) { return a * rsqrtf_(dot(a, a)); }
 YRT_HD float length(V3 a) { return sqrtf(dot(a, a)); }
 YRT_HD float reduce_max(V3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
