@@ -162,7 +162,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     acc = {"rays": 0.0, "closest": 0.0, "shadow": 0.0, "samples": 0.0, "msClosest": 0.0, "msShadow": 0.0,
-           "msShade": 0.0, "nClosest": 0.0, "nShadow": 0.0}
+           "msShade": 0.0, "nClosest": 0.0, "nShadow": 0.0, "msRender": 0.0, "msGather": 0.0}
     for _ in range(a.steps):
         st = step()
         acc["closest"] += st["raysClosest"]
@@ -173,6 +173,8 @@ def main():
         acc["msShade"] += st["msShade"]
         acc["nClosest"] += st["launchesClosest"]
         acc["nShadow"] += st["launchesShadow"]
+        acc["msRender"] += st["msRender"]
+        acc["msGather"] += st["msGather"]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -187,6 +189,7 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     rays, closest, shadow = tot.tolist()
     elapsed = tmax.item()
+    per_rank = rank_times(acc["msRender"] / a.steps, acc["msGather"] / a.steps, world, red_dev, gather)
 
     # one more frame, untimed, on one wavefront lane: no two kernels overlap, so its HIP-event
     # durations are each kernel's own (what a rocprof --kernel-trace summary averages); the
@@ -287,6 +290,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "gather": gather,
+            "per_rank": per_rank,
             "launcher": os.environ.get("YRT_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none"),
             "stereo_cubemap": stereo,
         }
@@ -297,6 +301,30 @@ def main():
         dist.destroy_process_group()
     if stereo and stereo.get("gather_check") not in (None, "bit_exact"):
         sys.exit(f"stereo cubemap gather check failed: {stereo['gather_check']}")
+
+
+def rank_times(render_ms, gather_ms, world, red_dev, gather):
+    """Per-rank diagnosis of an N-rank step: each rank's wall time until its tiles were
+    rendered and its gather time after that (YRTRenderStats msRender / msGather: the gather
+    includes waiting for the slowest rank), as max / mean / min over the ranks, so a weak scaling
+    curve says whether imbalance or the gather costs it."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([render_ms, gather_ms], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rows = [x.tolist() for x in allt]
+    else:
+        rows = [t.tolist()]
+    r = np.array([x[0] for x in rows])
+    g = np.array([x[1] for x in rows])
+    return {"render_ms": {"max": round(float(r.max()), 2), "mean": round(float(r.mean()), 2),
+                          "min": round(float(r.min()), 2), "imbalance": round(float(r.max() / max(r.mean(), 1e-9)), 4)},
+            "gather_ms": {"max": round(float(g.max()), 2), "mean": round(float(g.mean()), 2),
+                          "min": round(float(g.min()), 2)},
+            "gather_path": gather,
+            "note": "per timed step; render = this rank's tiles rendered, gather = after that (waits for peers)"}
 
 
 def physical_gpus(world, local):
@@ -461,9 +489,13 @@ def stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used):
                 faces_t[f].copy_(torch.from_numpy(rgb8_rows(img, stride)))
             dist.reduce(faces_t, dst=0, op=dist.ReduceOp.SUM)
         st = dev.render_stats()
+        cube_ms[0] += st["msRender"]
+        cube_ms[1] += st["msGather"]
         return st["raysClosest"] + st["raysShadow"]
 
+    cube_ms = [0.0, 0.0]
     one_cube()  # untimed: allocations, sample table
+    cube_ms = [0.0, 0.0]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -496,7 +528,9 @@ def stereo_cubemap(a, dev, rank, world, backend, gather, local, gpus_used):
            "ms_per_cubemap_min": round(per[0] * 1e3, 1),
            "samples_per_s": round(samples / dt, 1), "frames": a.stereo_frames,
            "parallelism": f"cube-tiles-roundrobin{world}", "gather": "C++ RCCL" if cxx else "torch reduce",
-           "gather_check": None}
+           "gather_check": None,
+           "per_rank": rank_times(cube_ms[0] / a.stereo_frames, cube_ms[1] / a.stereo_frames, world,
+                                  "cuda" if backend == "nccl" else "cpu", gather)}
     if world > 1:
         # the gathered cubemap (rank 0) against a one-GPU render of the same cubemap
         got = None

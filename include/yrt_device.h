@@ -163,6 +163,8 @@ typedef struct YRTRenderStats {
   double nodeVisits;      /* reserved (0): visit counts come from oracle_count_visits */
   double triVisits;
   double gather;          /* how the frame was gathered: YRT_GATHER_* */
+  double msRender;        /* wall time until this process's tiles were rendered (multi-GPU diagnosis) */
+  double msGather;        /* wall time of the gather after that (0 without one; includes waiting for peers) */
 } YRTRenderStats;
 #define YRT_GATHER_NONE 0           /* one device, no gather */
 #define YRT_GATHER_D2D 1            /* logical shards of one GPU: device-to-device copy */

@@ -394,6 +394,7 @@ void fb_read_back(FrameBufferObj& F, int id) {
 void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& S, ToneMapperObj& T,
                     const std::vector<FrameBufferObj*>& F, int accumulate) {
   auto t0 = std::chrono::steady_clock::now();
+  auto tRendered = t0;  // this process's tiles rendered (before any gather)
   // A process-level gather (yrtSetShardComm) is collective: every rank must reach it, so any
   // failure of this rank's part (arguments, scene, kernels) is reported to the peers through
   // the status exchange at its start instead of being thrown past it.
@@ -468,6 +469,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
     shardZero = !procGather && (nr == 1 || shardCount > 1);
     if (nr == 1) {
       render_shard(*ctx[0], *scenes[0], R, C, T, W, H, shardIndex, shardCount, accumulate, true);
+      tRendered = std::chrono::steady_clock::now();
     } else {
       // device k of this process renders the tiles t = shardIndex + k * shardCount (mod shardCount * N)
       std::vector<std::string> errs(nr);
@@ -484,6 +486,7 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
       for (auto& t : th) t.join();
       for (auto& e : errs)
         if (!e.empty()) throw std::runtime_error(e);
+      tRendered = std::chrono::steady_clock::now();
       gatherPath = gather_local(base, numTiles);
     }
   } catch (const std::exception& e) {
@@ -530,7 +533,11 @@ void Device::render(RendererObj& R, const std::vector<CameraObj*>& C, SceneObj& 
   }
   stats.samples = ctx[0]->stats.samples;
   stats.gather = gatherPath;
-  stats.msTotal = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const auto tEnd = std::chrono::steady_clock::now();
+  if (tRendered == t0) tRendered = tEnd;  // the render threw before its end (collective error path)
+  stats.msTotal = std::chrono::duration<double, std::milli>(tEnd - t0).count();
+  stats.msRender = std::chrono::duration<double, std::milli>(tRendered - t0).count();
+  stats.msGather = std::chrono::duration<double, std::milli>(tEnd - tRendered).count();
   status(R, 2, 1.f);
 }
 

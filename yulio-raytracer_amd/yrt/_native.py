@@ -43,7 +43,8 @@ PF = C.POINTER(C.c_float)
 class RenderStats(C.Structure):
     _fields_ = [(n, C.c_double) for n in (
         "raysClosest", "raysShadow", "samples", "msTotal", "msTraceClosest", "msTraceShadow", "msShade",
-        "msOther", "launchesClosest", "launchesShadow", "nodeVisits", "triVisits", "gather")]
+        "msOther", "launchesClosest", "launchesShadow", "nodeVisits", "triVisits", "gather", "msRender",
+        "msGather")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
