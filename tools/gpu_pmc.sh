@@ -14,9 +14,16 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 i=0
+# VALU lane utilization: thread-cycles of VALU work per VALU instruction cycle, if
+# this rocprofv3 lists the counter on gfx950 (rocprofv3 -L), normalized by the calibration
+# kernel's (every lane active) in tools/pmc_json.py
+LANE=""
+cd /tmp && timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1
+grep -q "SQ_THREAD_CYCLES_VALU" $OUT/counters.txt && LANE="SQ_THREAD_CYCLES_VALU"
+echo "lane counter: ${LANE:-none listed}"
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT" \
-           "TCC_HIT_sum TCC_MISS_sum"; do
+           "TCC_HIT_sum TCC_MISS_sum" ${LANE:+"$LANE SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE"}; do
   i=$((i+1))
   cd /tmp && timeout -k 10 -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
      python3 $R/bench.py --steps 1 --warmup 0 --capture 0 --no-cpu-baseline $ARGS > $OUT/p$i.log 2>&1
@@ -24,7 +31,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
-cd /tmp && timeout -k 10 -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
+cd /tmp && timeout -k 10 -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT $LANE \
    --output-format csv -d $OUT/calib -o run -- $R/tools/valu_calib > $OUT/calib.log 2>&1
 rc=$?; echo "calib rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/calib.log; exit $rc; }
 cd $R && python3 tools/pmc_json.py $OUT $OUT/pmc.json > /dev/null && echo "pmc.json written"

@@ -65,6 +65,9 @@ def derive(c):
         d["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS)
     if "TCC_HIT_sum" in c and (c["TCC_HIT_sum"] + c.get("TCC_MISS_sum", 0)) > 0:
         d["l2_hit"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU"):
+        # thread-cycles per VALU instruction cycle; / the calibration kernel's (64 active lanes)
+        d["thread_cycles_per_valu_cycle"] = c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"]
     if c.get("SQ_WAVE_CYCLES"):
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in c:
@@ -82,11 +85,23 @@ def main(root, out):
                 config = json.loads(line)["config"]
     kern = {k: derive(v) for k, v in per_dispatch(passes).items() if k != "k_valu_calib"}
     calib = per_dispatch([root / "calib"]).get("k_valu_calib") if (root / "calib").exists() else None
+    full = derive(calib).get("thread_cycles_per_valu_cycle") if calib else None
+    if full:
+        # VALU lane utilization: active lanes per issued VALU cycle, relative to a kernel whose
+        # every lane is active; useful_valu_frac = valu_busy x lane utilization
+        for k, v in kern.items():
+            if "thread_cycles_per_valu_cycle" in v:
+                v["valu_lane_util"] = v["thread_cycles_per_valu_cycle"] / full
+                if "valu_busy" in v:
+                    v["useful_valu_frac"] = v["valu_busy"] * v["valu_lane_util"]
     res = {"source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh), bench.py --steps 1 "
                      "--warmup 0 --capture 0 --no-cpu-baseline",
            "formulas": {"hbm_bytes_per_dispatch": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
                         "valu_busy": f"4*SQ_ACTIVE_INST_VALU / ({SIMDS} SIMDs * GRBM_GUI_ACTIVE/{XCDS})",
-                        "l2_hit": "TCC_HIT_sum/(TCC_HIT_sum+TCC_MISS_sum)"},
+                        "l2_hit": "TCC_HIT_sum/(TCC_HIT_sum+TCC_MISS_sum)",
+                        "valu_lane_util": "(SQ_THREAD_CYCLES_VALU/SQ_ACTIVE_INST_VALU) / the same ratio of the "
+                                          "calibration kernel (all 64 lanes active)",
+                        "useful_valu_frac": "valu_busy * valu_lane_util"},
            "config": config, "kernels": kern,
            "calibration": derive(calib) if calib else None}
     Path(out).write_text(json.dumps(res, indent=1) + "\n")

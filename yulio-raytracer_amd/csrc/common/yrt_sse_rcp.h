@@ -23,8 +23,10 @@
  *
  * Both are computed here exactly, so the GPU (v_rcp_f32 based) and the host (IEEE division)
  * produce the same bits and neither depends on the CPU vendor:
- *   rcp:   q = RN(2^25 / D), D = 4097 + 2i odd; the estimate q0 is within one of q and
- *          2*(2^25 - q0*D) in (-D, D] decides (no ties: D is odd);
+ *   rcp:   RN(1/mid) in float (correctly rounded on both sides), rounded to 12 bits, with
+ *          the one entry where that double rounding differs corrected (see yrt_rcpps); an exact
+ *          integer form (q = RN(2^25 / D), D = 4097 + 2i, one multiply to check the remainder)
+ *          measured ~8 VALU more per call;
  *   rsqrt: q = RN(8192 / sqrt(A / 2048)), A = (2049 + 2j) << p; the estimate q0 is within one
  *          of q, and q is right iff (2q - 1)^2 A < 2^39 < (2q + 1)^2 A (never equal: A's odd
  *          part is > 1), i.e. iff the high 32 bits of the 64-bit products are < 128 and >= 128:
@@ -57,10 +59,12 @@ YRT_SSE_FN float yrt_sse_float(uint32_t u) {
   return f;
 }
 
-/* an estimate of 1/x for x in [4097, 8191]: any value within a few ulp will do */
-YRT_SSE_FN float yrt_sse_rcp_est(float x) {
+/* RN(1/x) for x in [1, 2): the hardware estimate plus one FMA Newton step is correctly rounded
+ * there on gfx950 (rcp_rn in yrt_math.h, checked on all 2^32 inputs by yrtDebugCheckMath) */
+YRT_SSE_FN float yrt_sse_rcp_rn(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_rcpf(x);
+  const float y = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
 #else
   return 1.0f / x;
 #endif
@@ -76,14 +80,18 @@ YRT_SSE_FN float yrt_sse_rsq_est(float x) {
 /* the high 32 bits of a 32 x 32-bit product (one v_mul_hi_u32 on gfx950) */
 YRT_SSE_FN uint32_t yrt_sse_mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
-/* Intel rcpps (one lane) */
+/* Intel rcpps (one lane): RN(1/mid) rounded to 12 mantissa bits. mid = the input's top 11
+ * mantissa bits + a half unit, exponent 0; 1/mid lies in (0.5, 1), so the 12-bit rounding is an
+ * add of half a unit and a mask on its bits. That double rounding (24 then 12 bits) matches the
+ * direct one on 2047 of the 2048 entries; entry 1984 rounds up across the tie-free midpoint and is
+ * corrected (tests/test_sse_rcp.py, ref_check_sse_exhaustive, yrtDebugCheckMathTable). */
 YRT_SSE_FN float yrt_rcpps(float x) {
   const uint32_t u = yrt_sse_bits(x), s = u & 0x80000000u, e = (u >> 23) & 0xffu;
-  const int D = 4097 + 2 * (int)((u >> 12) & 0x7ffu);
-  int q = (int)(33554432.0f * yrt_sse_rcp_est((float)D) + 0.5f);
-  const int r2 = 2 * (33554432 - q * D); /* exact: q*D < 2^27 */
-  q += (r2 > D) - (r2 < -D);
-  uint32_t out = s | ((253u - e) << 23) | ((uint32_t)(q - 4096) << 11);
+  const uint32_t mid = (u & 0x7ff000u) | 0x3f800800u;
+  uint32_t y = yrt_sse_bits(yrt_sse_rcp_rn(yrt_sse_float(mid)));  /* exponent 126 */
+  y = (y + 0x400u) & 0x7ff800u;
+  y -= (mid == 0x3ffc0800u) ? 0x800u : 0u;                       /* entry 1984 */
+  uint32_t out = s | ((253u - e) << 23) | y;
   if (e >= 253u) out = s;                                             /* below 2^-126: +-0 */
   if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : s;         /* NaN stays (quiet), inf -> 0 */
   if (e == 0u) out = s | 0x7f800000u;                                 /* +-0, subnormal -> +-inf */
@@ -99,40 +107,14 @@ YRT_SSE_FN uint32_t yrt_rsqrtps_m(uint32_t p, uint32_t j) {
   return (uint32_t)(q - 4096);
 }
 
-#if defined(__HIPCC__) && defined(__cplusplus)
-/* On the GPU the 2048 mantissas are a 4 KB table in the code object, built at compile time
- * with the same integer test (a binary search for the q with (2q-1)^2 A < 2^39 < (2q+1)^2 A):
- * the arithmetic form's temporaries cost the camera-ray code 20 VGPRs (k_raygen 59 -> 79) and
- * the fused depth-0 trace kernel 60 B of scratch. Equal to yrt_rsqrtps_m for every entry
- * (the exhaustive GPU check against the Intel tables covers all of them). */
-struct YrtRsqTab {
-  unsigned short m[2048];
-};
-constexpr YrtRsqTab yrt_make_rsq_tab() {
-  YrtRsqTab t{};
-  for (unsigned i = 0; i < 2048; ++i) {
-    const unsigned long long A = (2049ull + 2ull * (i & 1023u)) << (i >> 10);
-    unsigned lo = 4096, hi = 8192; /* largest q with (2q - 1)^2 A < 2^39 */
-    while (lo < hi) {
-      const unsigned mid = (lo + hi + 1) / 2;
-      if ((2ull * mid - 1) * (2ull * mid - 1) * A < (1ull << 39)) lo = mid; else hi = mid - 1;
-    }
-    t.m[i] = (unsigned short)(lo - 4096);
-  }
-  return t;
-}
-__device__ static constexpr YrtRsqTab yrt_rsq_tab = yrt_make_rsq_tab();
-#endif
 
 /* Intel rsqrtps (one lane) */
 YRT_SSE_FN float yrt_rsqrtps(float x) {
   const uint32_t u = yrt_sse_bits(x), e = (u >> 23) & 0xffu;
   const int E = (int)e - 127, p = E & 1, k = (E - p) / 2;
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(YRT_RSQ_ARITH)
-  const uint32_t m = yrt_rsq_tab.m[((uint32_t)p << 10) | ((u >> 13) & 0x3ffu)];
-#else
+  /* (a 4 KB table of the 2048 mantissas in the code object measured 0.6 % slower on C3 and C4:
+   * a dependent load where this is ~12 VALU, profiles/r06/ab_r06a.txt) */
   const uint32_t m = yrt_rsqrtps_m((uint32_t)p, (u >> 13) & 0x3ffu);
-#endif
   uint32_t out = ((uint32_t)(126 - k) << 23) | (m << 11);
   if (u & 0x80000000u) out = 0xffc00000u;                             /* negative: default NaN */
   if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : ((u & 0x80000000u) ? 0xffc00000u : 0u);

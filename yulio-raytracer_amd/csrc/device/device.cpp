@@ -170,7 +170,7 @@ struct GpuCtx {
         L.qThr[k].alloc(Q * 16);
       }
       L.hit.alloc(Q * 16);
-      L.hitGeom.alloc(Q * 4);
+      if (trace_hit_geom()) L.hitGeom.alloc(Q * 4);
       L.pathL.alloc(Q * 16);
       L.pathCap = Q;
     }

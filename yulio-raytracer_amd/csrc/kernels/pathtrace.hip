@@ -418,6 +418,14 @@ __device__ unsigned long long g_traceProfile[8];
 #ifndef YRT_NODE_BIAS
 #define YRT_NODE_BIAS 8  // node step iff lanes at a node * 4 > blocked lanes * YRT_NODE_BIAS
 #endif
+// The closest-hit kernels can store each hit's geometry id (hitGeom) so that k_shade loads the
+// geometry record beside the shading record instead of after it (one dependent level fewer).
+// Measured same box (profiles/r06/ab_r06a.txt): k_shade 2.663 ms per launch with it, 2.617
+// without, C3 and C4 within the spread: the 4-byte store and load per ray cost what the shorter
+// chain saves. Off by default; -DYRT_HIT_GEOM=1 for the A/B.
+#ifndef YRT_HIT_GEOM
+#define YRT_HIT_GEOM 0
+#endif
 // Node format per traversal kind: 1 = the 64-B quantized nodes (common/yrt_qnode.h), 0 = the
 // 128-B float nodes. Both give the same query results bit for bit (conservative boxes).
 #ifndef YRT_QNODES_ANY
@@ -599,7 +607,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
         pr.qOrg[slot] = ro;
         pr.qDir[slot] = rd;
         hitOut[slot] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri));
-        occOut[slot] = bestGeom;
+        if (YRT_HIT_GEOM && occOut) occOut[slot] = bestGeom;
       }
       m &= ~sub;
     }
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
       prim_store();                                                                                  \
     else {                                                                                           \
       hitOut[q] = make_float4(best.t, best.u / bestDen, best.v / bestDen, __int_as_float(best.tri)); \
-      if (occOut) occOut[q] = bestGeom;                                                              \
+      if (YRT_HIT_GEOM && occOut) occOut[q] = bestGeom;                                              \
     }                                                                                                \
     q = -1;                                                                                          \
   } while (0)
@@ -856,7 +864,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             const bool ok = g & (t > r.tnear) & ((t < best.t + 0.0f) | tie);
             if (ok & (k < lTake)) {
               best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
-              bestGeom = __float_as_int(tt[k].e2[3]);
+              if (YRT_HIT_GEOM) bestGeom = __float_as_int(tt[k].e2[3]);
             }
           }
         }
@@ -876,7 +884,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
             }
             if (ok) {
               best.t = t; best.u = U; best.v = V; bestDen = absDen; best.tri = gid;
-              bestGeom = __float_as_int(tr.e2[3]);
+              if (YRT_HIT_GEOM) bestGeom = __float_as_int(tr.e2[3]);
             }
           }
         }
@@ -1439,7 +1447,7 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
     if (active) {
       path = pb.qPath[cur][q];
       h = pb.hit[q];
-#ifndef YRT_NO_HIT_GEOM
+#if YRT_HIT_GEOM
       hg = pb.hitGeom[q];
 #endif
       if (depthLevel == 0) {
@@ -1516,10 +1524,10 @@ __global__ __launch_bounds__(YRT_BLOCK) __attribute__((amdgpu_waves_per_eu(
       rec = fv.pixelSets[pixelId] * rp.spp + s;
       // the geometry id comes with the hit (k_trace's hitGeom), so its record is loaded beside
       // the shading record: hit -> {shading record, geometry record} -> texels
-#ifdef YRT_NO_HIT_GEOM
-      g = __float_as_int(r0.w);  // (A/B: the geometry id of the shading record, one level later)
-#else
+#if YRT_HIT_GEOM
       g = hg;
+#else
+      g = __float_as_int(r0.w);  // geometry id rides in the shading record
 #endif
       const GpuGeomRec& gr = sv.geomRecs[g];
       const int mat = gr.g.material;
@@ -1873,6 +1881,7 @@ void launch_raygen(const FrameView& fv, const PathBuffers& pb, const BatchInfo& 
 // geometry id
 void launch_trace_closest(const SceneView& sv, const float4* org, const float4* dir, const unsigned* counts,
                           int numSegs, int segCap, float4* hit, hipStream_t s, const float* time, int* hitGeom) {
+  if (!YRT_HIT_GEOM) hitGeom = nullptr;
   const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   if (time)
     hipLaunchKernelGGL((k_trace<false, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs, segCap,
@@ -1883,6 +1892,7 @@ void launch_trace_closest(const SceneView& sv, const float4* org, const float4* 
 }
 
 void launch_trace_primary(const SceneView& sv, const PrimaryRays& pr, float4* hit, int* hitGeom, hipStream_t s) {
+  if (!YRT_HIT_GEOM) hitGeom = nullptr;
   const dim3 grid(grid_for(pr.numPaths, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   hipLaunchKernelGGL((k_trace<false, false, 1>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, (const float4*)nullptr,
                      (const float4*)nullptr, (const unsigned*)nullptr, 0, 0, hit, hitGeom, sv.traceSpill,
@@ -2285,6 +2295,8 @@ __global__ __launch_bounds__(YRT_BLOCK) void k_quantize_nodes(const GpuNode* __r
   yrt_quantize_node(nodes[i], q);  // the host builder's function: the same bytes
   qnodes[i] = q;
 }
+
+bool trace_hit_geom() { return YRT_HIT_GEOM != 0; }
 
 int trace_node_bytes(bool anyHit) {
   return (anyHit ? YRT_QNODES_ANY : YRT_QNODES_CLOSEST) ? (int)sizeof(GpuQNode) : (int)sizeof(GpuNode);

@@ -213,6 +213,8 @@ void launch_refit_nodes(GpuNode* nodes, const GpuTri* tris, const int4* indices,
 void launch_quantize_nodes(const GpuNode* nodes, GpuQNode* qnodes, int count, hipStream_t s);
 // bytes per node of the closest-hit / any-hit traversal as built (YRT_QNODES_CLOSEST / _ANY)
 int trace_node_bytes(bool anyHit);
+// whether the closest-hit kernels store each hit's geometry id (YRT_HIT_GEOM)
+bool trace_hit_geom();
 void launch_debug_render(const SceneView& sv, const FrameView& fv, int maxDepth, int spp, int numTiles, float* fbFloat,
                          uint8_t* fbRGB8, int rgb8Stride, hipStream_t s);
 
