@@ -1,0 +1,15 @@
+# round-6 batch D: where the reference reciprocals cost on C4 — one-lane kernel stats of the C4
+# cube job (tools/cube_shard_time.py C4 --mode cube --gpus 1) for the default build and the
+# round-5 reciprocals (ieee), and of C3 for both.
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+R=$GRAFT_REPO_ROOT
+for v in head ieee; do
+  envs=""; [ $v != head ] && envs="YRT_LIB_DIR=$R/yulio-raytracer_amd/lib_variants/$v"
+  cd /tmp && env $envs YRT_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4l1_${v}_r06d -o run -- \
+    python3 $R/tools/cube_shard_time.py C4 --mode cube --gpus 1 > $R/gpurun_out/c4l1_${v}_r06d.log 2>&1 || exit $?
+  cd $R && python3 tools/kstats_csv.py gpurun_out/prof_c4l1_${v}_r06d 8 > gpurun_out/kstats_c4l1_${v}_r06d.txt 2>&1; echo "== C4 $v"; head -8 gpurun_out/kstats_c4l1_${v}_r06d.txt
+  cd /tmp && env $envs YRT_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3l1_${v}_r06d -o run -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 2 --capture 0 > $R/gpurun_out/c3l1_${v}_r06d.json 2>&1 || exit $?
+  cd $R && python3 tools/kstats_csv.py gpurun_out/prof_c3l1_${v}_r06d 8 > gpurun_out/kstats_c3l1_${v}_r06d.txt 2>&1; echo "== C3 $v"; head -6 gpurun_out/kstats_c3l1_${v}_r06d.txt
+done
