@@ -13,3 +13,8 @@ for v in head ieee; do
     python3 $R/bench.py --no-cpu-baseline --steps 2 --capture 0 > $R/gpurun_out/c3l1_${v}_r06d.json 2>&1 || exit $?
   cd $R && python3 tools/kstats_csv.py gpurun_out/prof_c3l1_${v}_r06d 8 > gpurun_out/kstats_c3l1_${v}_r06d.txt 2>&1; echo "== C3 $v"; head -6 gpurun_out/kstats_c3l1_${v}_r06d.txt
 done
+for v in head ieee; do
+  envs=""; [ $v != head ] && envs="YRT_LIB_DIR=$R/yulio-raytracer_amd/lib_variants/$v"
+  cd $R && env $envs timeout -k 10 300 python tools/c5_bench.py --spp 128 --no-face --no-startrt --no-cpu --out gpurun_out/c5_d_$v.json > gpurun_out/c5_d_$v.log 2>&1 || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/c5_d_$v.json')); print('$v C5 128spp', d['render_cube_job'])" | cut -c1-300
+done
