@@ -46,3 +46,8 @@ def test_gpus_two_without_launcher(tmp_path):
     line = json.loads(lines[0])
     assert line["ranks"] == 2 and line["launcher"].startswith("bench.py --gpus")
     assert line["stereo_cubemap"]["gather_check"] == "bit_exact"
+    # the N > 1 diagnosis: each rank's render and gather time, max / mean / min
+    for pr in (line["per_rank"], line["stereo_cubemap"]["per_rank"]):
+        r_ms, g_ms = pr["render_ms"], pr["gather_ms"]
+        assert 0 < r_ms["min"] <= r_ms["mean"] <= r_ms["max"] and r_ms["imbalance"] >= 1.0
+        assert 0 <= g_ms["min"] <= g_ms["mean"] <= g_ms["max"] and pr["gather_path"]

@@ -87,6 +87,9 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="0: the config's own (C4 256, C5 1024)")
     ap.add_argument("--out", default="")
     ap.add_argument("--capacity", type=int, default=0, help="paths per wavefront batch (0: device default)")
+    ap.add_argument("--reps", type=int, default=3,
+                    help="timed renders per share; its time is their median (one render of a ~50 ms share "
+                         "varies by a few ms from run to run, and the max over ranks picks that noise up)")
     a = ap.parse_args()
     spp = a.spp or {"C3": 64, "C4": 256, "C5": 1024}[a.cfg]
     if a.cfg == "C3" and a.size == 1536:
@@ -101,6 +104,7 @@ def main():
     for n in [int(x) for x in a.gpus.split(",")]:
         ranks = range(n) if a.ranks == "all" else [int(r) for r in a.ranks.split(",") if int(r) < n]
         times = {}
+        spread = {}
         rays = 0.0
         if n > 1:  # untimed: the share's batch size reallocates the path queues once
             dev.set_tile_shard(0, n)
@@ -113,18 +117,27 @@ def main():
                 # not hold) already hold zeros outside the share (device.cpp FrameBlock::zeroKey)
                 for _ in range(2):
                     render_cube(ses, a.cfg, a.mode)
-            t = time.perf_counter()
-            rays += render_cube(ses, a.cfg, a.mode)
-            times[r] = time.perf_counter() - t
-            print(f"{a.cfg} {a.mode} N={n} rank {r}: {times[r] * 1e3:.1f} ms", flush=True)
+            reps = []
+            for _ in range(max(1, a.reps)):
+                t = time.perf_counter()
+                rays_r = render_cube(ses, a.cfg, a.mode)
+                reps.append(time.perf_counter() - t)
+            rays += rays_r
+            times[r] = sorted(reps)[len(reps) // 2]
+            spread[r] = (min(reps), max(reps))
+            print(f"{a.cfg} {a.mode} N={n} rank {r}: {times[r] * 1e3:.1f} ms (median of {len(reps)}: "
+                  f"{', '.join(f'{x * 1e3:.1f}' for x in reps)})", flush=True)
         tmax = max(times.values())
         if n == 1:
             t1 = tmax
         row = {"config": a.cfg, "mode": a.mode, "capacity": a.capacity or "default", "n": n, "ranks_timed": list(times), "ms_max": round(tmax * 1e3, 1),
                "ms_mean": round(sum(times.values()) / len(times) * 1e3, 1),
                "ms_per_rank": {str(k): round(v * 1e3, 1) for k, v in times.items()},
+               "ms_per_rank_min_max": {str(k): [round(v[0] * 1e3, 1), round(v[1] * 1e3, 1)] for k, v in spread.items()},
+               "reps": a.reps, "max_over_mean": round(tmax / (sum(times.values()) / len(times)), 4),
                "predicted_efficiency": round(t1 / (n * tmax), 3) if t1 else None,
                "Mrays_per_s_per_gpu": round(rays / sum(times.values()) / 1e6, 1)}
+        # (the per-rank time is the median of --reps renders; rays are those of the last one)
         rows.append(row)
         print(json.dumps(row), flush=True)
     dev.set_tile_shard(0, 1)
