@@ -245,6 +245,13 @@ def main():
                 "avg_launch_ms_overlapped": round(avg_ms_overlapped, 4),
                 "valu_ceiling": (pmc or {}).get("calibration", {}).get("valu_busy") if pmc else None,
                 "valu_ceiling_note": "the same formula on a pure-FMA kernel at 8 waves/SIMD (tools/valu_calib.hip)",
+                # busy counts issue cycles, not active lanes
+                "valu_lane_util": _r4(kp.get("valu_lane_util")),
+                "useful_valu_frac": _r4(kp.get("useful_valu_frac")),
+                "lane_util_by_kernel": {k: {"valu_busy": _r4(v.get("valu_busy")), "valu_lane_util": _r4(v.get("valu_lane_util")),
+                                            "useful_valu_frac": _r4(v.get("useful_valu_frac"))}
+                                        for k, v in (pmc or {}).get("kernels", {}).items()
+                                        if k in ("k_trace<false>", "k_trace<true>", "k_shade")} or None,
                 "hbm": {"achieved": round(hbm_gbs, 1) if hbm_gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
                         "bytes_per_launch": round(traffic) if traffic else None},
@@ -301,6 +308,10 @@ def main():
         dist.destroy_process_group()
     if stereo and stereo.get("gather_check") not in (None, "bit_exact"):
         sys.exit(f"stereo cubemap gather check failed: {stereo['gather_check']}")
+
+
+def _r4(x):
+    return round(x, 4) if isinstance(x, (int, float)) else None
 
 
 def rank_times(render_ms, gather_ms, world, red_dev, gather):

@@ -1,6 +1,7 @@
 # round-6 batch D: where the reference reciprocals cost on C4 — one-lane kernel stats of the C4
 # cube job (tools/cube_shard_time.py C4 --mode cube --gpus 1) for the default build and the
-# round-5 reciprocals (ieee), and of C3 for both.
+# round-5 reciprocals (ieee), and of C3 for both; then the bench A/B head / ieee / rsqint (the
+# batch-B rsqrtps: v_rsq estimate + 64-bit integer check) twice.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
@@ -18,3 +19,4 @@ for v in head ieee; do
   cd $R && env $envs timeout -k 10 300 python tools/c5_bench.py --spp 128 --no-face --no-startrt --no-cpu --out gpurun_out/c5_d_$v.json > gpurun_out/c5_d_$v.log 2>&1 || exit $?
   python3 -c "import json; d=json.load(open('gpurun_out/c5_d_$v.json')); print('$v C5 128spp', d['render_cube_job'])" | cut -c1-300
 done
+bash tools/gpu_ab_cfg.sh r06d "head|-|" "ieee|ieee|" "rsqint|rsqint|" "head2|-|" "ieee2|ieee|" "rsqint2|rsqint|" || exit $?

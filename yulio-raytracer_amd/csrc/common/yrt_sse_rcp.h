@@ -27,10 +27,9 @@
  *          the one entry where that double rounding differs corrected (see yrt_rcpps); an exact
  *          integer form (q = RN(2^25 / D), D = 4097 + 2i, one multiply to check the remainder)
  *          measured ~8 VALU more per call;
- *   rsqrt: q = RN(8192 / sqrt(A / 2048)), A = (2049 + 2j) << p; the estimate q0 is within one
- *          of q, and q is right iff (2q - 1)^2 A < 2^39 < (2q + 1)^2 A (never equal: A's odd
- *          part is > 1), i.e. iff the high 32 bits of the 64-bit products are < 128 and >= 128:
- *          one 32-bit multiply-high per side.
+ *   rsqrt: RN(1 / RN(sqrt(mid))) in float, both correctly rounded on both sides, rounded to
+ *          12 bits: equal to the direct rounding on every entry (the closest call is 9e-5 of
+ *          a unit from a tie).
  * Exhaustive checks: against the host's rcpps/rsqrtps over all 2^32 inputs
  * (tests/test_ref_pin.py, Intel hosts), the GPU against the committed tables over all 2^32
  * inputs (yrtDebugCheckMathTable, tests/test_gpu_parity.py).
@@ -69,17 +68,6 @@ YRT_SSE_FN float yrt_sse_rcp_rn(float x) {
   return 1.0f / x;
 #endif
 }
-/* an estimate of 1/sqrt(x) for x in [1, 4) */
-YRT_SSE_FN float yrt_sse_rsq_est(float x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_rsqf(x);
-#else
-  return 1.0f / __builtin_sqrtf(x);
-#endif
-}
-/* the high 32 bits of a 32 x 32-bit product (one v_mul_hi_u32 on gfx950) */
-YRT_SSE_FN uint32_t yrt_sse_mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
-
 /* Intel rcpps (one lane): RN(1/mid) rounded to 12 mantissa bits. mid = the input's top 11
  * mantissa bits + a half unit, exponent 0; 1/mid lies in (0.5, 1), so the 12-bit rounding is an
  * add of half a unit and a mask on its bits. That double rounding (24 then 12 bits) matches the
@@ -98,24 +86,31 @@ YRT_SSE_FN float yrt_rcpps(float x) {
   return yrt_sse_float(out);
 }
 
-/* the rsqrtps mantissa m = q - 4096 of table entry (p << 10) | j */
-YRT_SSE_FN uint32_t yrt_rsqrtps_m(uint32_t p, uint32_t j) {
-  const uint32_t A = (2049u + 2u * j) << p;
-  int q = (int)(8192.0f * yrt_sse_rsq_est((float)A * (1.0f / 2048.0f)) + 0.5f);
-  const uint32_t lo = (uint32_t)(2 * q - 1), hi = (uint32_t)(2 * q + 1); /* < 2^15: squares fit */
-  q += (yrt_sse_mulhi(hi * hi, A) < 128u) - (yrt_sse_mulhi(lo * lo, A) >= 128u);
-  return (uint32_t)(q - 4096);
+/* RN(sqrt(x)) for x in [1, 4): the hardware square root (within an ulp) corrected by the signs
+ * of the two neighbours' FMA residuals (LLVM's correctly rounded f32 sqrt, without its
+ * subnormal scaling, which this range does not need) */
+YRT_SSE_FN float yrt_sse_sqrt_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = yrt_sse_float(yrt_sse_bits(s) - 1u), sup = yrt_sse_float(yrt_sse_bits(s) + 1u);
+  float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+  r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+  return r;
+#else
+  return __builtin_sqrtf(x);
+#endif
 }
-
-
-/* Intel rsqrtps (one lane) */
+/* Intel rsqrtps (one lane): RN(1 / RN(sqrt(mid))) rounded to 12 mantissa bits, mid = the input's
+ * top 10 mantissa bits + a half unit, times 2^p (exponent parity); that double rounding matches
+ * the direct one on all 2048 entries (tests/test_sse_rcp.py, exhaustive checks). An exact integer
+ * form (a v_rsq estimate checked by (2q -+ 1)^2 A against 2^39) needs two 64-bit multiply-adds,
+ * quarter-rate instructions. */
 YRT_SSE_FN float yrt_rsqrtps(float x) {
   const uint32_t u = yrt_sse_bits(x), e = (u >> 23) & 0xffu;
   const int E = (int)e - 127, p = E & 1, k = (E - p) / 2;
-  /* (a 4 KB table of the 2048 mantissas in the code object measured 0.6 % slower on C3 and C4:
-   * a dependent load where this is ~12 VALU, profiles/r06/ab_r06a.txt) */
-  const uint32_t m = yrt_rsqrtps_m((uint32_t)p, (u >> 13) & 0x3ffu);
-  uint32_t out = ((uint32_t)(126 - k) << 23) | (m << 11);
+  const uint32_t mid = ((uint32_t)(127 + p) << 23) | (u & 0x7fe000u) | 0x1000u;
+  const uint32_t y = (yrt_sse_bits(yrt_sse_rcp_rn(yrt_sse_sqrt_rn(yrt_sse_float(mid)))) + 0x400u) & 0x7ff800u;
+  uint32_t out = ((uint32_t)(126 - k) << 23) | y;
   if (u & 0x80000000u) out = 0xffc00000u;                             /* negative: default NaN */
   if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : ((u & 0x80000000u) ? 0xffc00000u : 0u);
   if (e == 0u) out = (u & 0x80000000u) | 0x7f800000u;                 /* +-0, subnormal -> +-inf */
