@@ -5,6 +5,9 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/pytest_gpu_r06d.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_r06d.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu_r06d.log
 for v in head ieee; do
   envs=""; [ $v != head ] && envs="YRT_LIB_DIR=$R/yulio-raytracer_amd/lib_variants/$v"
   cd /tmp && env $envs YRT_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c4l1_${v}_r06d -o run -- \
