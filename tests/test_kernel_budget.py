@@ -41,4 +41,7 @@ def test_shade_kernels_hold_four_waves(res):
         if "8339454" in name:  # the generic every-material instantiation (2 waves, rare scenes)
             continue
         assert r["vgpr"] <= 128, (name, r)
-        assert r["scratch"] <= 16, (name, r)
+        # round 6: no scratch at all (round 5's 12 / 16 B in C4's and the Collada set's
+        # instantiations sat in rcp_rn's IEEE-division fallback, which the reference's rcp
+        # sequence, yrt_sse_rcp.h, does not have)
+        assert r["scratch"] == 0, (name, r)
