@@ -142,7 +142,10 @@ _sig(dev, "yrtSetKernelTiming", i32, vp, i32)
 _sig(dev, "yrtSetLanes", i32, vp, i32)
 _sig(dev, "yrtGetSceneInfo", i32, vp, vp, C.POINTER(SceneInfo))
 _sig(dev, "yrtExportBVH", i32, vp, vp, vp, sz, vp, sz)
-_sig(dev, "yrtExportQuantizedBVH", i32, vp, vp, vp, sz)
+try:  # round 6; absent from older builds selected with YRT_LIB_DIR (same-box A/B against round 5)
+    _sig(dev, "yrtExportQuantizedBVH", i32, vp, vp, vp, sz)
+except AttributeError:
+    pass
 _sig(dev, "yrtExportFrame", C.c_int64, vp, vp, vp, vp, vp, sz)
 _sig(dev, "yrtSetFrameSeed", i32, vp, C.c_uint32)
 _sig(dev, "yrtSetBatchCapacity", i32, vp, C.c_int64)
