@@ -915,6 +915,224 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+#if YRT_ANY2
+// ---------------------------------------------------------------- any hit, two rays per lane
+// k_occluded2: the shadow query of k_trace<true, false> (the same quantized box test, the same
+// farthest-child-first order, the same triangle test, so the same occlusion answers) with TWO
+// independent rays per lane. A node step loads both rays' nodes before testing either, a leaf
+// step both rays' triangles, so each lane keeps two dependent load -> test -> push chains in
+// flight. Round 5 measured this on the 128-B float nodes (k_occluded): 146 VGPRs, 3 waves/SIMD,
+// frame -2.7 %; the 64-B quantized node is 14 words instead of 28 per ray. Each ray slot has a
+// YRT_ANY2_LDS-entry LDS ring (2 x 16 x 256 B = 8 KB per wave, the one-ray kernel's LDS);
+// older entries spill to global memory. Slots without work load node 0 / triangle 0 (L2 hits)
+// so the loads stay unconditional and issue back to back.
+#ifndef YRT_ANY2_REFILL
+#define YRT_ANY2_REFILL 64  // refill when this many of the wave's 128 ray slots are idle
+#endif
+#ifndef YRT_ANY2_BIAS
+#define YRT_ANY2_BIAS 20  // node step iff slots at a node * 4 > blocked slots * YRT_ANY2_BIAS
+#endif
+#ifndef YRT_ANY2_WAVES
+#define YRT_ANY2_WAVES 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(YRT_ANY2_WAVES))) void k_occluded2(
+    SceneView sv, const float4* __restrict__ org, const float4* __restrict__ dir, const unsigned* __restrict__ counts,
+    int numSegs, int segCap, int* __restrict__ occOut, int* __restrict__ spillBuf, ShadowFuse sf) {
+  constexpr int R = YRT_ANY2_LDS;
+  __shared__ int lstack[2 * R * 64];
+  __shared__ QMap qm;
+  qmap_load(qm, counts, numSegs);
+  const unsigned n = qm.pre[YRT_QSEGS];
+  const int lane = lane_id();
+  unsigned chunk = (n + gridDim.x - 1) / gridDim.x;
+  chunk = chunk < 128u ? 128u : chunk;
+  unsigned next = blockIdx.x * chunk;
+  const unsigned end = min(n, next + chunk);
+  if (next >= end) return;  // wave-uniform
+
+  const GpuQNode* __restrict__ qnodes = sv.qnodes;
+  const GpuTri* __restrict__ tris = sv.tris;
+  int* stack = lstack + lane;
+  // spilled entries: [entry][slot][thread] (YRT_TRACE_SPILL_INTS covers 2 x (YRT_STACK_DEPTH - R)
+  // entries per thread of a 64-lane block)
+  const size_t spillStride = (size_t)gridDim.x * 64;
+  int* __restrict__ spill = spillBuf + blockIdx.x * 64 + lane;
+#define A2_SLOT(s, i) ((((s) * R) + ((i) & (R - 1))) * 64)
+#define A2_SPILL(s, i) spill[((size_t)((i) - R) * 2 + (s)) * spillStride]
+#define A2_PUSH(s, e)                                              \
+  do {                                                             \
+    if (sp[s] >= R) A2_SPILL(s, sp[s]) = stack[A2_SLOT(s, sp[s])]; \
+    stack[A2_SLOT(s, sp[s])] = (e);                                \
+    sp[s] += 1;                                                    \
+  } while (0)
+#define A2_POP(s)                                                          \
+  do {                                                                     \
+    if (sp[s] == 0) {                                                      \
+      cur[s] = -1;                                                         \
+    } else {                                                               \
+      sp[s] -= 1;                                                          \
+      cur[s] = stack[A2_SLOT(s, sp[s])];                                   \
+      if (sp[s] >= R) stack[A2_SLOT(s, sp[s])] = A2_SPILL(s, sp[s]);       \
+    }                                                                      \
+  } while (0)
+  // per slot: the ray (org.xyz, tnear | dir.xyz, tfar | inv.xyz, plane offsets), its query
+  // index, stack pointer, current entry (index << 5 | count; count 0 = inner node, -1 = stack
+  // exhausted) and a parked leaf (0 = none). The slab constants org * inv and margin are
+  // recomputed per step instead of held in four more registers per slot.
+  float4 ro[2], rd[2], ri[2];
+  int q[2], sp[2], cur[2], pend[2];
+  bool has[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    ro[s] = rd[s] = ri[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+    q[s] = sp[s] = pend[s] = 0;
+    cur[s] = -1;
+    has[s] = false;
+  }
+  auto ray_of = [&](int s) {
+    RayPre r;
+    r.org = v3(ro[s].x, ro[s].y, ro[s].z);
+    r.dir = v3(rd[s].x, rd[s].y, rd[s].z);
+    r.inv = v3(ri[s].x, ri[s].y, ri[s].z);
+    r.tnear = ro[s].w;
+    r.tfar = rd[s].w;
+    ray_slab_consts(r.org, r.inv, r.oi, r.margin);
+    return r;
+  };
+#define A2_INNER(s) (cur[s] >= 0 && (cur[s] & 31) == 0)
+#define A2_NNODE() (__popcll(ballot(A2_INNER(0)) & hasB0) + __popcll(ballot(A2_INNER(1)) & hasB1))
+#define A2_NBLOCKED()                                                       \
+  (__popcll(ballot(!A2_INNER(0) && (pend[0] != 0 || cur[0] > 0)) & hasB0) + \
+   __popcll(ballot(!A2_INNER(1) && (pend[1] != 0 || cur[1] > 0)) & hasB1))
+  while (true) {
+    // retire slots whose traversal is complete (unoccluded)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (has[s] && cur[s] < 0 && pend[s] == 0) {
+        shadow_done(sf, occOut, q[s], false);
+        has[s] = false;
+      }
+    const unsigned long long idle0 = ballot(!has[0]), idle1 = ballot(!has[1]);
+    const int nIdle0 = __popcll(idle0);
+    const int nIdle = nIdle0 + __popcll(idle1);
+    if (nIdle >= YRT_ANY2_REFILL) {
+      if (next < end) {
+        // idle slot 0s take the next rays of the chunk in lane order, then idle slot 1s
+        bool take[2];
+        float4 lo[2], ld[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const unsigned li = next + (s ? (unsigned)nIdle0 : 0u) + (unsigned)lanes_below(s ? idle1 : idle0);
+          take[s] = !has[s] && li < end;
+          if (take[s]) {
+            q[s] = qmap_phys(qm, segCap, li);
+            lo[s] = org[q[s]];
+            ld[s] = dir[q[s]];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          if (take[s]) {
+            ro[s] = lo[s];
+            rd[s] = ld[s];
+            ri[s] = make_float4(safe_inv(rd[s].x), safe_inv(rd[s].y), safe_inv(rd[s].z), 0.f);
+            ri[s].w = __int_as_float(plane_offsets(ri[s].x, ri[s].y, ri[s].z));
+            sp[s] = 0;
+            cur[s] = 0;
+            pend[s] = 0;
+            // NaN tfar (tMaxShadowRay = inf): nothing to traverse, unoccluded
+            has[s] = rd[s].w >= ro[s].w;
+            if (!has[s]) shadow_done(sf, occOut, q[s], false);
+          }
+        next += (unsigned)nIdle;
+      } else if (nIdle == 128) {
+        break;
+      }
+    }
+    // node steps while more slots can descend than are blocked on a leaf, else a leaf step
+    // (the one-ray kernel's rule, counted over both slots)
+    const unsigned long long hasB0 = ballot(has[0]), hasB1 = ballot(has[1]);
+    if (A2_NNODE() * 4 > A2_NBLOCKED() * YRT_ANY2_BIAS) {
+      while (true) {
+        bool act[2];
+        QNodeData nd[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          act[s] = has[s] && A2_INNER(s);
+          nd[s] = qnode_load(qnodes, act[s] ? (cur[s] >> 5) : 0);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const RayPre r = ray_of(s);
+          float t[4];
+          int c[4];
+          box4_qdata<true>(nd[s], r, __float_as_int(ri[s].w), r.tfar, t, c);
+          sort3_far(t, c);
+          if (act[s]) {
+            const float MISS = __int_as_float(0xff800000);
+            const int h3 = t[3] > MISS, h2 = t[2] > MISS, h1 = t[1] > MISS;
+            if (sp[s] + 3 <= R) {
+              // unconditional stores into free ring slots, sp advanced past the hit children
+              stack[A2_SLOT(s, sp[s])] = c[3];
+              stack[A2_SLOT(s, sp[s] + h3)] = c[2];
+              stack[A2_SLOT(s, sp[s] + h3 + h2)] = c[1];
+              sp[s] += h3 + h2 + h1;
+            } else {
+              if (h3) A2_PUSH(s, c[3]);
+              if (h2) A2_PUSH(s, c[2]);
+              if (h1) A2_PUSH(s, c[1]);
+            }
+            if (t[0] > MISS) cur[s] = c[0];
+            else A2_POP(s);
+            // a leaf reached while none is parked: park it and keep descending
+            if (cur[s] > 0 && (cur[s] & 31) != 0 && pend[s] == 0) {
+              pend[s] = cur[s];
+              A2_POP(s);
+            }
+          }
+        }
+        if (!(A2_NNODE() * 4 > A2_NBLOCKED() * YRT_ANY2_BIAS)) break;
+      }
+    } else {
+      // leaf step: one triangle per slot, the parked leaf or else the current entry
+      int lf[2];
+      bool usePend[2];
+      GpuTri tr[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        usePend[s] = pend[s] != 0;
+        lf[s] = !has[s] ? 0 : usePend[s] ? pend[s] : (cur[s] > 0 && (cur[s] & 31) != 0) ? cur[s] : 0;
+        tr[s] = tris[lf[s] > 0 ? (lf[s] >> 5) : 0];
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (lf[s] > 0) {
+          const RayPre r = ray_of(s);
+          float t, U, V, absDen;
+          const bool found = tri_test_t(tr[s], r, r.tfar, t, U, V, absDen);
+          // the leaf's next triangle (index + 1, count - 1), or the leaf is done
+          const int rest = (lf[s] & 31) > 1 ? lf[s] + 31 : 0;
+          if (usePend[s]) pend[s] = rest;
+          else if (rest) cur[s] = rest;
+          else A2_POP(s);
+          if (found) {
+            shadow_done(sf, occOut, q[s], true);
+            has[s] = false;
+          }
+        }
+      }
+    }
+  }
+#undef A2_INNER
+#undef A2_NNODE
+#undef A2_NBLOCKED
+#undef A2_SLOT
+#undef A2_SPILL
+#undef A2_PUSH
+#undef A2_POP
+}
+#endif  // YRT_ANY2
+
 // ---------------------------------------------------------------- shading helpers
 // BackendSceneFlat::postIntersect -> Shape::postIntersect
 // geom: the hit triangle's geometry record (sv.geoms / the geometry part of sv.geomRecs)
@@ -1903,6 +2121,13 @@ void launch_trace_any(const SceneView& sv, const float4* org, const float4* dir,
                       int segCap, int* occluded, hipStream_t s, const ShadowFuse* fuse, const float* time) {
   const dim3 grid(grid_for((long long)numSegs * segCap, YRT_TRACE_BLOCK, YRT_TRACE_GRID));
   const ShadowFuse sf = fuse ? *fuse : ShadowFuse{};
+#if YRT_ANY2
+  if (!time) {
+    hipLaunchKernelGGL(k_occluded2, grid, dim3(64), 0, s, sv, org, dir, counts, numSegs, segCap, occluded,
+                       sv.traceSpill, sf);
+    return;
+  }
+#endif
   if (time)
     hipLaunchKernelGGL((k_trace<true, true>), grid, dim3(YRT_TRACE_BLOCK), 0, s, sv, org, dir, counts, numSegs,
                        segCap, (float4*)nullptr, occluded, sv.traceSpill, sf, time, PrimaryRays{});

@@ -50,7 +50,12 @@ struct SceneView {
 #ifndef YRT_TRACE_GRID
 #define YRT_TRACE_GRID 16384
 #endif
-#define YRT_TRACE_SPILL_INTS ((size_t)YRT_TRACE_GRID * YRT_TRACE_BLOCK * (YRT_STACK_DEPTH - YRT_LDS_STACK_MIN))
+// spilled stack entries per lane: the one-ray kernels' (YRT_STACK_DEPTH - ring), or two ray slots'
+// of k_occluded2 (one 64-lane wave per block, YRT_TRACE_GRID blocks at most)
+#define YRT_SPILL_1 (YRT_STACK_DEPTH - YRT_LDS_STACK_MIN)
+#define YRT_SPILL_2 (YRT_ANY2 ? 2 * (YRT_STACK_DEPTH - YRT_ANY2_LDS) : 0)
+#define YRT_TRACE_SPILL_INTS \
+  ((size_t)YRT_TRACE_GRID * (YRT_TRACE_BLOCK > 64 ? YRT_TRACE_BLOCK : 64) * (YRT_SPILL_1 > YRT_SPILL_2 ? YRT_SPILL_1 : YRT_SPILL_2))
 
 struct FrameView {
   const GpuRenderParams* rp;   // device copy

@@ -35,6 +35,13 @@ static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be
 #endif
 static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
 #define YRT_LDS_STACK_MIN (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
+#ifndef YRT_ANY2
+#define YRT_ANY2 0  // 1: static scenes' shadow queries run two rays per lane (k_occluded2)
+#endif
+#ifndef YRT_ANY2_LDS
+#define YRT_ANY2_LDS 16  // LDS ring entries per ray slot of k_occluded2
+#endif
+static_assert((YRT_ANY2_LDS & (YRT_ANY2_LDS - 1)) == 0, "YRT_ANY2_LDS must be a power of two");
 #ifndef YRT_TRACE_BLOCK
 // one wave per block (8 KB of LDS stack): +1.0 % on C3 over 128-lane blocks once the trace code
 // was scheduled for a 6-wave target (profiles/r01/variants_r01.txt)
@@ -203,15 +210,38 @@ __device__ __forceinline__ void box4_data(const NodeData& d, const RayPre& r, fl
 // at least one quantum outside the float node's child boxes, which covers a's rounding (see
 // yrt_qnode.h), so the same boxes are never culled and every query returns the same bits.
 // Empty slots are tested by their child reference.
+// The quantized node as loaded (14 words).
+struct QNodeData {
+  float4 h;   // origin xyz, quantum exponents
+  int4 ch;
+  uint4 pa;   // lo x, hi x, lo y, hi y
+  uint2 pb;   // lo z, hi z
+};
+__device__ __forceinline__ QNodeData qnode_load(const GpuQNode* __restrict__ base, int nodeIdx) {
+  const char* b0 = (const char*)base + ((unsigned)nodeIdx << 6);
+  QNodeData d;
+  d.h = *(const float4*)b0;
+  d.ch = *(const int4*)(b0 + 16);
+  d.pa = *(const uint4*)(b0 + 32);
+  d.pb = *(const uint2*)(b0 + 48);
+  return d;
+}
+template <bool ANY>
+__device__ __forceinline__ void box4_qdata(const QNodeData& d, const RayPre& r, int planeOff, float tmax, float t[4],
+                                           int c[4]);
 template <bool ANY>
 __device__ __forceinline__ void box4_quant(const RayPre& r, int planeOff, float tmax, float t[4], int c[4],
                                            const GpuQNode* __restrict__ base, int nodeIdx) {
+  box4_qdata<ANY>(qnode_load(base, nodeIdx), r, planeOff, tmax, t, c);
+}
+template <bool ANY>
+__device__ __forceinline__ void box4_qdata(const QNodeData& d, const RayPre& r, int planeOff, float tmax, float t[4],
+                                           int c[4]) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-  const char* b0 = (const char*)base + ((unsigned)nodeIdx << 6);
-  const float4 h = *(const float4*)b0;
-  const int4 ch = *(const int4*)(b0 + 16);
-  const uint4 pa = *(const uint4*)(b0 + 32);   // lo x, hi x, lo y, hi y
-  const uint2 pb = *(const uint2*)(b0 + 48);   // lo z, hi z
+  const float4 h = d.h;
+  const int4 ch = d.ch;
+  const uint4 pa = d.pa;
+  const uint2 pb = d.pb;
   const uint32_t ex = __float_as_uint(h.w);
   const float sx = __uint_as_float((ex & 0xffu) << 23) * r.inv.x;
   const float sy = __uint_as_float(((ex >> 8) & 0xffu) << 23) * r.inv.y;
