@@ -31,7 +31,11 @@
 #endif
 static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
 #ifndef YRT_LDS_STACK_ANY
-#define YRT_LDS_STACK_ANY YRT_LDS_STACK  // LDS ring of the any-hit (shadow) instantiation
+// LDS ring of the any-hit (shadow) instantiation: 16 entries (4.2 KB per wave). On the 64-B
+// quantized nodes that kernel needs 72 VGPRs, so with 32 entries (8.3 KB) LDS held it at 4.75
+// waves/SIMD and with 16 registers allow 7: same box (profiles/r06/ab_r06f.txt) C5 -5.0 %, C4
+// -1 %, C3 +0.2 %. (On the float nodes, at 5 waves either way, 16 entries were 3.3 % slower.)
+#define YRT_LDS_STACK_ANY 16
 #endif
 static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
 #define YRT_LDS_STACK_MIN (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
