@@ -73,16 +73,30 @@ YRT_SSE_FN float yrt_sse_rcp_rn(float x) {
  * add of half a unit and a mask on its bits. That double rounding (24 then 12 bits) matches the
  * direct one on 2047 of the 2048 entries; entry 1984 rounds up across the tie-free midpoint and is
  * corrected (tests/test_sse_rcp.py, ref_check_sse_exhaustive, yrtDebugCheckMathTable). */
+/* The inputs outside the normal range (exponent 0, or >= 253 for rcpps; negative, zero,
+ * subnormal, inf or NaN for rsqrtps) are rare on the render path: on the GPU their selects run
+ * only when some lane of the wave has one (a ballot and a uniform branch, one VALU instead of
+ * about ten per call). */
+#ifndef YRT_SSE_BRANCH
+#define YRT_SSE_BRANCH 0  /* bit 0: rcpps, bit 1: rsqrtps (A/B switch; both cost shade scratch) */
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define YRT_SSE_ANY(bit, c) (!(YRT_SSE_BRANCH & (bit)) || __builtin_amdgcn_ballot_w64(c) != 0)
+#else
+#define YRT_SSE_ANY(bit, c) 1
+#endif
 YRT_SSE_FN float yrt_rcpps(float x) {
   const uint32_t u = yrt_sse_bits(x), s = u & 0x80000000u, e = (u >> 23) & 0xffu;
   const uint32_t mid = (u & 0x7ff000u) | 0x3f800800u;
   uint32_t y = yrt_sse_bits(yrt_sse_rcp_rn(yrt_sse_float(mid)));  /* exponent 126 */
   y = (y + 0x400u) & 0x7ff800u;
   y -= (mid == 0x3ffc0800u) ? 0x800u : 0u;                       /* entry 1984 */
-  uint32_t out = s | ((253u - e) << 23) | y;
-  if (e >= 253u) out = s;                                             /* below 2^-126: +-0 */
-  if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : s;         /* NaN stays (quiet), inf -> 0 */
-  if (e == 0u) out = s | 0x7f800000u;                                 /* +-0, subnormal -> +-inf */
+  uint32_t out = s | ((253u - e) << 23) | y;                          /* e in [1, 252] */
+  if (YRT_SSE_ANY(1, e - 1u > 251u)) {
+    if (e >= 253u) out = s;                                           /* below 2^-126: +-0 */
+    if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : s;       /* NaN stays (quiet), inf -> 0 */
+    if (e == 0u) out = s | 0x7f800000u;                               /* +-0, subnormal -> +-inf */
+  }
   return yrt_sse_float(out);
 }
 
@@ -110,10 +124,12 @@ YRT_SSE_FN float yrt_rsqrtps(float x) {
   const int E = (int)e - 127, p = E & 1, k = (E - p) / 2;
   const uint32_t mid = ((uint32_t)(127 + p) << 23) | (u & 0x7fe000u) | 0x1000u;
   const uint32_t y = (yrt_sse_bits(yrt_sse_rcp_rn(yrt_sse_sqrt_rn(yrt_sse_float(mid)))) + 0x400u) & 0x7ff800u;
-  uint32_t out = ((uint32_t)(126 - k) << 23) | y;
-  if (u & 0x80000000u) out = 0xffc00000u;                             /* negative: default NaN */
-  if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : ((u & 0x80000000u) ? 0xffc00000u : 0u);
-  if (e == 0u) out = (u & 0x80000000u) | 0x7f800000u;                 /* +-0, subnormal -> +-inf */
+  uint32_t out = ((uint32_t)(126 - k) << 23) | y;                     /* positive, e in [1, 254] */
+  if (YRT_SSE_ANY(2, u - 0x00800000u >= 0x7f000000u)) {
+    if (u & 0x80000000u) out = 0xffc00000u;                           /* negative: default NaN */
+    if (e == 255u) out = (u & 0x7fffffu) ? (u | 0x400000u) : ((u & 0x80000000u) ? 0xffc00000u : 0u);
+    if (e == 0u) out = (u & 0x80000000u) | 0x7f800000u;               /* +-0, subnormal -> +-inf */
+  }
   return yrt_sse_float(out);
 }
 

@@ -453,7 +453,10 @@ __device__ unsigned long long g_traceProfile[8];
 #define YRT_TRACE_WAVES_PRIM 5
 #endif
 #ifndef YRT_TRACE_WAVES_ANY
-#define YRT_TRACE_WAVES_ANY YRT_TRACE_WAVES  // occupancy target of the shadow-ray instantiation
+// occupancy target of the shadow-ray instantiation: 8 waves/SIMD (64 VGPRs, no scratch; the
+// 16-entry LDS ring allows 9): same box against 7 (profiles/r06/ab_r06g.txt) C3 +1.9 / +0.8 %,
+// C4 -0.7 / -1.1 %, C5 -1.4 %
+#define YRT_TRACE_WAVES_ANY 8
 #endif
 // A finished shadow query: the occlusion flag, or (fused, PathBuffers::fuseShadow) the
 // light's contribution added to its path's radiance when unoccluded (k_shadow_resolve order).
