@@ -509,7 +509,7 @@ __global__ __launch_bounds__(YRT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu
                                                          ShadowFuse sf, const float* __restrict__ rayTime,
                                                          PrimaryRays pr) {
   static_assert(!PRIM || (!ANY && !MOTION), "camera rays: closest hit, static scenes");
-  constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : YRT_LDS_STACK;
+  constexpr int kLds = ANY ? YRT_LDS_STACK_ANY : PRIM ? YRT_LDS_STACK_PRIM : YRT_LDS_STACK;
   __shared__ int lstack[kLds * YRT_TRACE_BLOCK];
   __shared__ QMap qm;
   unsigned n;

@@ -38,7 +38,12 @@ static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be
 #define YRT_LDS_STACK_ANY 16
 #endif
 static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
-#define YRT_LDS_STACK_MIN (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
+#ifndef YRT_LDS_STACK_PRIM
+#define YRT_LDS_STACK_PRIM YRT_LDS_STACK  // LDS ring of the fused depth-0 (camera ray) instantiation
+#endif
+static_assert((YRT_LDS_STACK_PRIM & (YRT_LDS_STACK_PRIM - 1)) == 0, "YRT_LDS_STACK_PRIM must be a power of two");
+#define YRT_LDS_STACK_MIN2 (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
+#define YRT_LDS_STACK_MIN (YRT_LDS_STACK_MIN2 < YRT_LDS_STACK_PRIM ? YRT_LDS_STACK_MIN2 : YRT_LDS_STACK_PRIM)
 #ifndef YRT_ANY2
 #define YRT_ANY2 0  // 1: static scenes' shadow queries run two rays per lane (k_occluded2)
 #endif
