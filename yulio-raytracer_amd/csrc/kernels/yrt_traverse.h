@@ -13,9 +13,10 @@
 //   closest hit: smallest (t, global triangle id) — order independent, so any BVH gives
 //   the same answer (used to pin the GPU against the oracle's own BVH).
 // Stack: per-lane short stack in LDS, [depth][lane] so a wave's pushes hit 64 distinct
-// banks. Only YRT_LDS_STACK entries live in LDS (32 x 256 B per wave: 8 KB per 64-lane
-// block, so LDS caps occupancy at 5 waves/SIMD); deeper entries spill to global memory.
-// 32 entries instead of 16: +4.9 % on C3 (the 16-entry ring spilled often enough to matter).
+// banks. Only the top entries live in LDS — a ring of YRT_LDS_STACK (32) for the queued
+// closest-hit kernels (8 KB per 64-lane block), 16 for the any-hit and the fused depth-0 kernels
+// (round 6, see their macros below); deeper entries spill to global memory.
+// Closest hit, 32 entries instead of 16: +4.9 % on C3 in round 1, -2 % on C3 again in round 6.
 // The builder bounds the tree depth to YRT_STACK_DEPTH-1 (device/bvh_build.cpp).
 #pragma once
 
@@ -39,7 +40,11 @@ static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be
 #endif
 static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK_ANY must be a power of two");
 #ifndef YRT_LDS_STACK_PRIM
-#define YRT_LDS_STACK_PRIM YRT_LDS_STACK  // LDS ring of the fused depth-0 (camera ray) instantiation
+// LDS ring of the fused depth-0 (camera ray) instantiation: 16 entries. The kernel stays at 5
+// waves/SIMD (96 VGPRs) either way, but the 4 KB ring leaves LDS for the other lanes' kernels
+// running beside it: same box (profiles/r06/ab_r06i.txt) C4 -1.3 %, its N = 8 share -2 %, C3
+// and C5 within the spread. The queued closest-hit kernels keep 32 (16: C3 -2 %).
+#define YRT_LDS_STACK_PRIM 16
 #endif
 static_assert((YRT_LDS_STACK_PRIM & (YRT_LDS_STACK_PRIM - 1)) == 0, "YRT_LDS_STACK_PRIM must be a power of two");
 #define YRT_LDS_STACK_MIN2 (YRT_LDS_STACK < YRT_LDS_STACK_ANY ? YRT_LDS_STACK : YRT_LDS_STACK_ANY)
