@@ -17,7 +17,7 @@ def main():
     flags = subprocess.run(["make", "-s", "-C", str(PKG), "-pn"], capture_output=True, text=True).stdout
     hip = re.search(r"^HIPFLAGS := (.*)$", flags, re.M)
     cxx = re.search(r"^CXXFLAGS := (.*)$", flags, re.M)
-    env = {"OPT": "-O3", "EXTRA": "", "STACK": "64", "LDSSTACK": "32", "ARCH": "gfx950", "HIPEXTRA": ""}
+    env = {"OPT": "-O3", "EXTRA": "", "STACK": "64", "LDSSTACK": "16", "ARCH": "gfx950", "HIPEXTRA": ""}
     def expand(t):
         t = t.replace("$(CXXFLAGS)", cxx.group(1))
         for k, v in env.items():

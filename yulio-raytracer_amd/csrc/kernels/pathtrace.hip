@@ -428,11 +428,15 @@ __device__ unsigned long long g_traceProfile[8];
 #endif
 // Node format per traversal kind: 1 = the 64-B quantized nodes (common/yrt_qnode.h), 0 = the
 // 128-B float nodes. Both give the same query results bit for bit (conservative boxes).
+// Closest hit: neutral at a 32-entry LDS ring (LDS-bound 4.75 waves/SIMD); with a 16-entry ring
+// the quantized kernel runs 74 VGPRs at 6 waves/SIMD and the smaller node footprint pays for the
+// extra waves' cache interference that the float nodes lose to (same box, profiles/r06/
+// ab_r06j.txt: C3 +5.3 %, C4 -1.8 %, C5 -2.5 %; float nodes with the 16-entry ring C3 -2 %).
 #ifndef YRT_QNODES_ANY
 #define YRT_QNODES_ANY 1
 #endif
 #ifndef YRT_QNODES_CLOSEST
-#define YRT_QNODES_CLOSEST 0
+#define YRT_QNODES_CLOSEST 1
 #endif
 #ifndef YRT_NODE_BIAS_ANY
 #define YRT_NODE_BIAS_ANY 20  // any hit: 12 over 8 -1.7 % on C3, C5 within the spread (r03 anyk); 4 +2.4 %;

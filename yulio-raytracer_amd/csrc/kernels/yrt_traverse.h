@@ -13,10 +13,10 @@
 //   closest hit: smallest (t, global triangle id) — order independent, so any BVH gives
 //   the same answer (used to pin the GPU against the oracle's own BVH).
 // Stack: per-lane short stack in LDS, [depth][lane] so a wave's pushes hit 64 distinct
-// banks. Only the top entries live in LDS — a ring of YRT_LDS_STACK (32) for the queued
-// closest-hit kernels (8 KB per 64-lane block), 16 for the any-hit and the fused depth-0 kernels
-// (round 6, see their macros below); deeper entries spill to global memory.
-// Closest hit, 32 entries instead of 16: +4.9 % on C3 in round 1, -2 % on C3 again in round 6.
+// banks. Only the top entries live in LDS, a ring of 16 per lane (4 KB per 64-lane block) for
+// every traversal kind since round 6; deeper entries spill to global memory. History: closest
+// hit on the float nodes, 32 entries instead of 16: +4.9 % on C3 in round 1, still +2 % in
+// round 6; on the 64-B quantized nodes 16 entries win (6 waves/SIMD, C3 +5.3 %, pathtrace.hip).
 // The builder bounds the tree depth to YRT_STACK_DEPTH-1 (device/bvh_build.cpp).
 #pragma once
 
@@ -28,7 +28,7 @@
 #define YRT_STACK_DEPTH 64   // bound on traversal stack entries + 1 (device/bvh_build.cpp enforces it)
 #endif
 #ifndef YRT_LDS_STACK
-#define YRT_LDS_STACK 32     // top entries kept in LDS; deeper ones spill (power of two)
+#define YRT_LDS_STACK 16     // top entries kept in LDS; deeper ones spill (power of two); Makefile LDSSTACK
 #endif
 static_assert((YRT_LDS_STACK & (YRT_LDS_STACK - 1)) == 0, "YRT_LDS_STACK must be a power of two");
 #ifndef YRT_LDS_STACK_ANY
@@ -43,7 +43,7 @@ static_assert((YRT_LDS_STACK_ANY & (YRT_LDS_STACK_ANY - 1)) == 0, "YRT_LDS_STACK
 // LDS ring of the fused depth-0 (camera ray) instantiation: 16 entries. The kernel stays at 5
 // waves/SIMD (96 VGPRs) either way, but the 4 KB ring leaves LDS for the other lanes' kernels
 // running beside it: same box (profiles/r06/ab_r06i.txt) C4 -1.3 %, its N = 8 share -2 %, C3
-// and C5 within the spread. The queued closest-hit kernels keep 32 (16: C3 -2 %).
+// and C5 within the spread (on the float nodes, when the queued closest-hit kernels kept 32).
 #define YRT_LDS_STACK_PRIM 16
 #endif
 static_assert((YRT_LDS_STACK_PRIM & (YRT_LDS_STACK_PRIM - 1)) == 0, "YRT_LDS_STACK_PRIM must be a power of two");
