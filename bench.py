@@ -231,10 +231,11 @@ def main():
         pmc, pmc_note = load_pmc(a, sinfo, world)
         kp = (pmc or {}).get("kernels", {}).get(kname, {})
         traffic = kp.get("hbm_bytes_per_dispatch")
-        valu = kp.get("valu_busy")
+        valu = kp.get("valu_issue_frac")
         hbm_gbs = traffic / (avg_ms * 1e-3) / 1e9 if traffic and avg_ms > 0 else None
         roof = {"bound": "valu-issue", "achieved": round(valu, 4) if valu is not None else None, "peak": 1.0,
-                "unit": "VALU-busy fraction of SIMD cycles",
+                "unit": "fraction of the SIMDs' VALU issue cycles (2 per wave64 VALU instruction on a 32-wide "
+                        "SIMD; SQ_INSTS_VALU, tools/pmc_json.py)",
                 "frac": round(valu, 4) if valu is not None else None,
                 "traffic": round(traffic) if traffic else None,
                 "kernel": "k_trace_closest" if dom == "closest" else "k_trace_any",
@@ -243,12 +244,20 @@ def main():
                                        "avg_launch_ms_overlapped is the timed frames' HIP-event average, which includes "
                                        "the other lane's concurrent kernels") if serial else "timed frames (lanes overlap)",
                 "avg_launch_ms_overlapped": round(avg_ms_overlapped, 4),
-                "valu_ceiling": (pmc or {}).get("calibration", {}).get("valu_busy") if pmc else None,
-                "valu_ceiling_note": "the same formula on a pure-FMA kernel at 8 waves/SIMD (tools/valu_calib.hip)",
+                "valu_issue_note": ("a lower bound of the issue-cycle share: packed (v_pk_*) instructions take 4 "
+                                    "cycles and transcendentals 8; the packed-FMA calibration kernel "
+                                    "(tools/valu_calib.hip, 8 waves/SIMD) fills valu_calibration_packed of its "
+                                    "4-cycle issue slots"),
+                # rounds 2-6's headline formula (quad-cycles of SQ_ACTIVE_INST_VALU): 2x the issue
+                # cycles of unpacked code, so it can exceed 1; kept for comparison with their records
+                "valu_busy_quad": _r4(kp.get("valu_busy")),
+                "valu_calibration_packed": _r4((pmc or {}).get("calibration", {}).get("valu_busy")) if pmc else None,
                 # busy counts issue cycles, not active lanes
                 "valu_lane_util": _r4(kp.get("valu_lane_util")),
                 "useful_valu_frac": _r4(kp.get("useful_valu_frac")),
-                "lane_util_by_kernel": {k: {"valu_busy": _r4(v.get("valu_busy")), "valu_lane_util": _r4(v.get("valu_lane_util")),
+                "lane_util_by_kernel": {k: {"valu_issue_frac": _r4(v.get("valu_issue_frac")),
+                                            "valu_busy_quad": _r4(v.get("valu_busy")),
+                                            "valu_lane_util": _r4(v.get("valu_lane_util")),
                                             "useful_valu_frac": _r4(v.get("useful_valu_frac"))}
                                         for k, v in (pmc or {}).get("kernels", {}).items()
                                         if k in ("k_trace<false>", "k_trace<true>", "k_shade")} or None,

@@ -11,11 +11,20 @@ Per kernel, averaged over its dispatches:
       (MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports 1/2 of the bytes of 16-B-per-lane
       reads — the traversal's node/triangle/ray loads are dwordx4; WRITE_SIZE is exact for 16-B
       stores; the unit is kB)
-  valu_busy = 4 * SQ_ACTIVE_INST_VALU / (SIMDS * GRBM_GUI_ACTIVE / XCDS)
-      SQ_ACTIVE_INST_VALU counts quad-cycles (x4 -> cycles) summed over every SIMD;
-      GRBM_GUI_ACTIVE is the GPU-busy cycle count summed over the 8 XCDs (/8 -> cycles of the
-      dispatch); SIMDS = 256 CUs x 4. The calibration kernel (pure FMA stream at 8 waves/SIMD)
-      must read ~1 under the same formula: reported as calibration.valu_busy.
+  valu_issue_frac = 2 * SQ_INSTS_VALU / (SIMDS * GRBM_GUI_ACTIVE / XCDS)
+      the fraction of the SIMDs' VALU issue cycles the kernel's wave64 VALU instructions take,
+      at 2 cycles each (CDNA4 SIMDs are 32 lanes wide: MI355X_MICROARCH.md, `v_fma_f32` wave64
+      2 cyc); SQ_INSTS_VALU counts wave-level VALU instructions summed over the GPU (the
+      calibration kernel's count equals its instruction count exactly); GRBM_GUI_ACTIVE is the
+      GPU-busy cycle count summed over the 8 XCDs (/8 -> cycles of the dispatch); SIMDS = 256
+      CUs x 4. Packed (v_pk_*) instructions take 4 cycles and transcendentals 8, so for mixed
+      code this is a lower bound of the issue-cycle share.
+  valu_busy = 4 * SQ_ACTIVE_INST_VALU / (SIMDS * GRBM_GUI_ACTIVE / XCDS)   (rounds 2-6 headline)
+      SQ_ACTIVE_INST_VALU counts quad-cycles (x4 -> cycles). The calibration kernel
+      (tools/valu_calib.hip) compiles to v_pk_fma_f32 — 4 cycles per wave64 instruction — and
+      reads 0.83; for unpacked code the quad-cycle count is 2x the issue cycles, so this figure
+      overstates issue utilization up to 2x and can exceed 1 (the round-6 closest-hit kernel
+      reads 1.03). Kept for comparison with earlier rounds' records.
   l2_hit = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
 """
 import csv
@@ -63,6 +72,8 @@ def derive(c):
         d["hbm_bytes_per_dispatch"] = 2.0 * 1024.0 * c.get("FETCH_SIZE", 0.0) + 1024.0 * c.get("WRITE_SIZE", 0.0)
     if c.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in c:
         d["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS)
+    if c.get("GRBM_GUI_ACTIVE") and "SQ_INSTS_VALU" in c:
+        d["valu_issue_frac"] = 2.0 * c["SQ_INSTS_VALU"] / (SIMDS * c["GRBM_GUI_ACTIVE"] / XCDS)
     if "TCC_HIT_sum" in c and (c["TCC_HIT_sum"] + c.get("TCC_MISS_sum", 0)) > 0:
         d["l2_hit"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
     if c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU"):
@@ -88,20 +99,24 @@ def main(root, out):
     full = derive(calib).get("thread_cycles_per_valu_cycle") if calib else None
     if full:
         # VALU lane utilization: active lanes per issued VALU cycle, relative to a kernel whose
-        # every lane is active; useful_valu_frac = valu_busy x lane utilization
+        # every lane is active; useful_valu_frac = valu_issue_frac x lane utilization
         for k, v in kern.items():
             if "thread_cycles_per_valu_cycle" in v:
                 v["valu_lane_util"] = v["thread_cycles_per_valu_cycle"] / full
-                if "valu_busy" in v:
-                    v["useful_valu_frac"] = v["valu_busy"] * v["valu_lane_util"]
+                if "valu_issue_frac" in v:
+                    v["useful_valu_frac"] = v["valu_issue_frac"] * v["valu_lane_util"]
     res = {"source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh), bench.py --steps 1 "
                      "--warmup 0 --capture 0 --no-cpu-baseline",
            "formulas": {"hbm_bytes_per_dispatch": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024",
-                        "valu_busy": f"4*SQ_ACTIVE_INST_VALU / ({SIMDS} SIMDs * GRBM_GUI_ACTIVE/{XCDS})",
+                        "valu_issue_frac": f"2*SQ_INSTS_VALU / ({SIMDS} SIMDs * GRBM_GUI_ACTIVE/{XCDS}): 2 issue "
+                                           "cycles per wave64 VALU instruction on a 32-wide SIMD (lower bound: "
+                                           "packed ops take 4, transcendentals 8)",
+                        "valu_busy": f"4*SQ_ACTIVE_INST_VALU / ({SIMDS} SIMDs * GRBM_GUI_ACTIVE/{XCDS}) (quad-cycle "
+                                     "count; 2x the issue cycles of unpacked code, rounds 2-6 records)",
                         "l2_hit": "TCC_HIT_sum/(TCC_HIT_sum+TCC_MISS_sum)",
                         "valu_lane_util": "(SQ_THREAD_CYCLES_VALU/SQ_ACTIVE_INST_VALU) / the same ratio of the "
                                           "calibration kernel (all 64 lanes active)",
-                        "useful_valu_frac": "valu_busy * valu_lane_util"},
+                        "useful_valu_frac": "valu_issue_frac * valu_lane_util"},
            "config": config, "kernels": kern,
            "calibration": derive(calib) if calib else None}
     Path(out).write_text(json.dumps(res, indent=1) + "\n")
