@@ -280,6 +280,10 @@ YRT_API int yrtDebugCheckMath(YRTDevice dev, int fn, uint64_t* out2);
  * reconstruction from table2048 (the 12-bit mantissas of tests/golden/sse_rcp_tables.json) for
  * all 2^32 inputs. out2 as yrtDebugCheckMath. */
 YRT_API int yrtDebugCheckMathTable(YRTDevice dev, int fn, const uint16_t* table2048, uint64_t* out2);
+/* The image tile that logical tile t of a sharded job's frame of T tiles covers
+ * (common/yrt_tile_scatter.h: a fixed bijection of [0, T), used by the renderer and the gather
+ * whenever the tile stride is above 1). Host-side; -1 for t outside [0, T). */
+YRT_API int yrtDebugTileScatter(int t, int T);
 /* Parity debugging: out4 == NULL arms the capture of the per-sample radiance (the pathL terms
  * the resolve sums, in s order) of pixel id y*width+x (-1 disarms) of frame `frame` for the
  * following renders (buffer of maxSamples float4); out4 != NULL copies the captured samples

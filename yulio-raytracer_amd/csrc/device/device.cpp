@@ -5,6 +5,7 @@
 // IntegratorRenderer::renderFrame/RenderJob (renderers/integratorrenderer.cpp:63-185),
 // DebugRenderer (renderers/debugrenderer.cpp:66-140).
 #include "../../../include/yrt_device.h"
+#include "../common/yrt_tile_scatter.h"
 
 #include <string.h>
 #include <strings.h>
@@ -2064,6 +2065,11 @@ int yrtDebugCheckMathTable(YRTDevice dev, int fn, const uint16_t* table2048, uin
   if (check_math_table(fn, table2048, (unsigned long long*)out2) != 0) throw std::runtime_error("check_math_table failed");
   return 0;
   DEV_END(-1)
+}
+
+int yrtDebugTileScatter(int t, int T) {
+  if (T < 1 || t < 0 || t >= T) return -1;
+  return yrt_tile_scatter(t, T);
 }
 
 int yrtSetTileShard(YRTDevice dev, int index, int count) {

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <set>
 
+#include "../common/yrt_tile_scatter.h"
 #include "yrt_kernels.h"
 #include "yrt_shade.h"
 #include "yrt_traverse.h"
@@ -282,6 +283,8 @@ __device__ __forceinline__ bool batch_tile(const RP& rp, const BatchInfo& bi, in
     f = fastdiv(tile, rp.divTilesPerFrame);
     tile -= f * rp.tilesPerFrame;
   }
+  // sharded jobs: the logical tile's image tile (common/yrt_tile_scatter.h; slab_pixel agrees)
+  if (bi.tileStride > 1) tile = yrt_tile_scatter(tile, rp.tilesPerFrame);
   const int ty = fastdiv(tile, rp.divTilesX);
   x0 = (tile - ty * rp.numTilesX) * 16;
   y0 = ty * 16;
@@ -2225,6 +2228,7 @@ __device__ __forceinline__ bool slab_pixel(const SlabLayout& L, int i, int& f, i
   int t = L.tileOffset + (i >> 8) * L.tileStride;
   f = t / L.tilesPerFrame;
   t -= f * L.tilesPerFrame;
+  if (L.tileStride > 1) t = yrt_tile_scatter(t, L.tilesPerFrame);  // as batch_tile
   x = (t % ntx) * 16 + (i & 15);
   y = (t / ntx) * 16 + ((i >> 4) & 15);
   return x < L.width && y < L.height;

@@ -175,6 +175,10 @@ try:  # debug-only entry; absent from older tuning builds selected with YRT_LIB_
     _sig(dev, "yrtDebugPixelSamples", i32, vp, i32, i32, vp, i32)
 except AttributeError:
     pass
+try:  # round 6; absent from older tuning builds selected with YRT_LIB_DIR
+    _sig(dev, "yrtDebugTileScatter", i32, i32, i32)
+except AttributeError:
+    pass
 _sig(dev, "yrtDebugDecodeImage", i32, cstr, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), vp, sz)
 _sig(dev, "yrtDebugSampleTable", i32, i32, i32, i32, i32, i32, cstr, PF, sz)
 
