@@ -595,9 +595,10 @@ def single_gpu_cube(args, local, stride):
 
 def cpu_baseline(ses, a):
     """The oracle (CPU restatement of the reference path) on a bounded sample of the same frame
-    (same spp/depth/scene/camera): by default every a.cpu_tile_stride-th 16x16 tile (t % N == 0,
-    the multi-GPU tile split's shard 0), spread over the whole frame so its rays per sample are
-    the frame's; or a centred band of a.cpu_rows rows (--cpu-tile-stride 0). On every logical
+    (same spp/depth/scene/camera): by default the multi-GPU tile split's shard 0 of
+    a.cpu_tile_stride (logical tiles t % N == 0, which cover a pseudo-random 1/N of the image's
+    16x16 tiles, common/yrt_tile_scatter.h), spread over the whole frame so its rays per sample
+    are the frame's; or a centred band of a.cpu_rows rows (--cpu-tile-stride 0). On every logical
     core this process can use (the reference default numThreads=0 -> all cores,
     common/sys/taskscheduler.cpp:105): one worker thread per CPU of the affinity
     mask, capped at the cgroup CPU quota when one is set (the GPU box grants 16 CPUs of a
@@ -612,7 +613,8 @@ def cpu_baseline(ses, a):
     t = time.perf_counter()
     if a.cpu_tile_stride > 0:
         _, st = oracle.render_shard(blob, a.size, a.size, ses.info()["gamma"], 0, a.cpu_tile_stride, threads=threads)
-        what = f"16x16 tiles t % {a.cpu_tile_stride} == 0 of the {a.size}^2 frame"
+        what = (f"the 16x16 tiles of shard 0 of {a.cpu_tile_stride} (logical t % {a.cpu_tile_stride} == 0, "
+                f"scattered over the image) of the {a.size}^2 frame")
     else:
         y0 = (a.size - a.cpu_rows) // 2
         _, st = oracle.render(blob, a.size, a.size, ses.info()["gamma"], rect=(0, y0, a.size, y0 + a.cpu_rows),
@@ -623,8 +625,9 @@ def cpu_baseline(ses, a):
     # the oracle's sample count is the whole frame's; the sample's own is its pixels x spp
     tx, ty = (a.size + 15) // 16, (a.size + 15) // 16
     if a.cpu_tile_stride > 0:
-        px = sum(min(16, a.size - 16 * (t % tx)) * min(16, a.size - 16 * (t // tx))
-                 for t in range(0, tx * ty, a.cpu_tile_stride))
+        from yrt import _native as N
+        img = [N.dev.yrtDebugTileScatter(t, tx * ty) for t in range(0, tx * ty, a.cpu_tile_stride)]
+        px = sum(min(16, a.size - 16 * (t % tx)) * min(16, a.size - 16 * (t // tx)) for t in img)
     else:
         px = a.cpu_rows * a.size
     samples = float(px) * a.spp

@@ -7,6 +7,7 @@
 #include "../yulio-raytracer_amd/csrc/common/yrt_libm.h"
 /* the reference's rcp/rsqrt: Intel rcpps/rsqrtps emulated exactly + math.h's Newton step */
 #include "../yulio-raytracer_amd/csrc/common/yrt_sse_rcp.h"
+#include "../yulio-raytracer_amd/csrc/common/yrt_tile_scatter.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -2333,7 +2334,7 @@ typedef struct {
   const Camera* C;
   const uint8_t* sets;
   int width, height, x0, y0, x1, y1, ntx, nty;
-  int shardIndex, shardCount; /* only tiles with tile % shardCount == shardIndex */
+  int shardIndex, shardCount; /* only logical tiles with lt % shardCount == shardIndex */
   float gamma;
   uint32_t seed;
   float* out;
@@ -2348,9 +2349,12 @@ static void* worker(void* arg) {
   double nc = 0, ns = 0;
   const float rcpW = rcp((float)J->width), rcpH = rcp((float)J->height);
   for (;;) {
-    const int tile = __sync_fetch_and_add(&J->next, 1);
-    if (tile >= J->ntx * J->nty) break;
-    if (tile % J->shardCount != J->shardIndex) continue;
+    const int lt = __sync_fetch_and_add(&J->next, 1);
+    if (lt >= J->ntx * J->nty) break;
+    if (lt % J->shardCount != J->shardIndex) continue;
+    /* the product's deal (not the reference's): logical tile lt of a sharded frame covers image
+     * tile yrt_tile_scatter(lt, T), common/yrt_tile_scatter.h */
+    const int tile = J->shardCount > 1 ? yrt_tile_scatter(lt, J->ntx * J->nty) : lt;
     const int tx = (tile % J->ntx) * 16, ty = (tile / J->ntx) * 16;
     for (int dy = 0; dy < 16; dy++) {
       const int y = ty + dy;

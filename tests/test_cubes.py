@@ -20,6 +20,7 @@ import pytest
 import oracle
 import yrt
 from helpers import c4_args, parity
+from yrt import _native as N
 from yrt import frederick
 
 FPR = ["-tMaxShadowRay", "120", "-ambientlight", "0.83", "0.95", "0.98", "-depth", "10", "-toeIn"]
@@ -67,7 +68,8 @@ def test_cube_job_equals_face_loop_c4(gpu_device, capacity):
 @pytest.mark.gpu
 def test_cube_job_shards_compose(gpu_device):
     """The cube's tile sequence dealt round-robin over 3 shards: the shards' faces are disjoint
-    and sum to the whole cube (C4's 110,592 tiles dealt tile_id mod N)."""
+    and sum to the whole cube (C4's 110,592 tiles dealt tile_id mod N; logical
+    tile l of a face covers image tile yrt_tile_scatter(l, T), common/yrt_tile_scatter.h)."""
     s = yrt.Session(c4_args(80, 2) + ["-fb", "RGB_FLOAT32"], device=gpu_device)
     full = s.render_cube()
     parts = []
@@ -78,13 +80,15 @@ def test_cube_job_shards_compose(gpu_device):
     finally:
         gpu_device.set_tile_shard(0, 1)
     tpf = 5 * 5  # 80^2 -> 5 x 5 tiles per face
+    logical = {N.dev.yrtDebugTileScatter(l, tpf): l for l in range(tpf)}  # image tile -> logical
+    assert sorted(logical) == list(range(tpf))
     for f in range(12):
         assert np.array_equal(sum(p[f] for p in parts), full[f])
         for k in range(3):
             for t in range(tpf):
                 ty, tx = divmod(t, 5)
                 blk = parts[k][f][16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16]
-                mine = (f * tpf + t) % 3 == k
+                mine = (f * tpf + logical[t]) % 3 == k
                 assert mine or not blk.any(), (f, t, k)
     s.close()
 

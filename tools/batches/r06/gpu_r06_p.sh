@@ -15,3 +15,5 @@ grep '^{' gpurun_out/scaling_prediction_c3_r06p.txt | cut -c1-400
 timeout -k 10 300 python -u tools/cube_shard_time.py C4 --mode cube --reps 3 > gpurun_out/scaling_prediction_c4_r06p.txt 2>&1 || exit $?
 grep '^{' gpurun_out/scaling_prediction_c4_r06p.txt | cut -c1-400
 bash tools/gpu_ab_cfg.sh r06p "head|-|" "rr|rr|" || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/bench_r06p.json 2> gpurun_out/bench_r06p.err || { tail -20 gpurun_out/bench_r06p.err; exit 1; }
+cut -c1-300 gpurun_out/bench_r06p.json
