@@ -176,7 +176,7 @@ YRT_API int yrtGetRenderStats(YRTDevice dev, YRTRenderStats* out);
 /* 1 = bracket every kernel with HIP events (adds sync-free event records). */
 YRT_API int yrtSetKernelTiming(YRTDevice dev, int enable);
 /* Wavefront lanes (HIP streams whose batches overlap) of every render context, 1..4; 0 = the
- * default (4, or YRT_LANES). With one lane no two kernels of a frame overlap, so the kernel
+ * default (3, or YRT_LANES). With one lane no two kernels of a frame overlap, so the kernel
  * timings above are each kernel's own duration (bench.py's roofline uses such a frame). */
 YRT_API int yrtSetLanes(YRTDevice dev, int lanes);
 /* Scene info: triangles, geometries, BVH nodes, BVH depth, build seconds; numTriRefs = leaf

@@ -78,9 +78,12 @@ struct GpuCtx {
 #define YRT_MAX_LANES 4  // one HIP stream each; HIP gives a process 4 hardware queues by default
 #endif
   static constexpr int kMaxLanes = YRT_MAX_LANES;  // YRT_LANES may ask for up to this many
-  // four: C3 +1.4 %, C4 cube job -2 % (N = 8 share -1.5 %), C5 -0.5 % over two on the same box
-  // (profiles/r05/ab_lanes_r05q.txt); in rounds 1-2 two were +4 % over one, and more no better
-  static constexpr int kDefaultLanes = 4;
+  // three: a process gets 4 hardware queues (GPU_MAX_HW_QUEUES), and four lane streams plus the
+  // context's own stream (clears, copies, the gather) share them. Same box against four
+  // (profiles/r06/ab_r06r.txt): C3 +3.4 %, C4 cube job -1.7 %, C5 -2.7 %, N = 8 rank shares C3
+  // -13.5 % (slowest) and C4 -5 %. (Round 5: four over two C3 +1.4 %, ab_lanes_r05q.txt; rounds
+  // 1-2: two +4 % over one.)
+  static constexpr int kDefaultLanes = 3;
   static int default_lanes() {
     int lanes = kDefaultLanes;
     if (const char* e = getenv("YRT_LANES")) lanes = std::max(1, std::min(kMaxLanes, atoi(e)));
