@@ -1,5 +1,5 @@
 # round-6 batch O: trace grid (blocks per traversal launch) at the new occupancies (6 waves/SIMD
-# closest hit, 8 any hit): 32768 (g32k) and 8192 (g8k) against 16384. C3/C4 twice, C5 128 spp.
+# closest hit, 8 any hit, three lanes): 32768 (g32k) and 8192 (g8k) against 16384. C3/C4 twice, C5 128 spp.
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
