@@ -1,4 +1,4 @@
-# round-6 batch U: PMC passes of the final tree (three lanes) into profiles/pmc_c3.json, then the
+# round-6 batch U: PMC passes of the final tree (one lane, as the roofline frame) into profiles/pmc_c3.json, then the
 # default bench line reading them.
 export TMPDIR=/tmp
 mkdir -p gpurun_out

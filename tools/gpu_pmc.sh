@@ -8,6 +8,10 @@ export TMPDIR=/tmp
 # one frame, no warm-up: the depth-0 kernels the steady state uses on C3 (camera rays mostly hit,
 # so Device::render_shard picks k_raygen + the queued trace once it has measured that)
 export YRT_PRIMARY=${YRT_PRIMARY:-0}
+# one lane: the per-dispatch counts must describe the batches of the bench's one-lane roofline
+# frame (with three lanes a C3 frame splits into 6 batches instead of 4; the counters are
+# collected with kernels serialized either way)
+export YRT_LANES=${YRT_LANES:-1}
 TAG=${1:-dev}
 ARGS=${2:-""}
 R=$GRAFT_REPO_ROOT
